@@ -1,0 +1,300 @@
+"""Fused MI355X execution engine for :class:`llmtrain.models.gpt.GPT`.
+
+The engine runs a whole forward + loss, and later the whole backward, as one explicitly
+scheduled sequence of kernels instead of an autograd graph of small ops:
+
+forward (per block; ``M = B*T`` tokens, ``d`` model width, residual stream kept in fp32)::
+
+    x_s, h1  = add_layernorm(x, delta)            # HIP: residual add fused into LN, bf16 out
+    qkv      = h1 @ Wqkv^T + b                    # hipBLASLt (bias epilogue), bf16
+    att, lse = flash_attn_fwd(qkv)                # HIP: gfx950 MFMA, packed qkv, causal
+    y        = att @ Wo^T + b                     # hipBLASLt
+    x_m, h2  = add_layernorm(x_s, y)              # HIP
+    u        = h2 @ Wfc^T + b                     # hipBLASLt
+    g        = gelu(u)                            # HIP (exact erf GELU)
+    delta    = g @ Wproj^T + b                    # hipBLASLt  (added by the next LN)
+
+then ``ln_f`` (+ the last residual add), the tied LM head GEMM against a vocab-padded bf16
+shadow (50257 → 50304 rows) and a fused softmax-cross-entropy kernel that produces the per-row
+loss AND overwrites the logits with their gradient in the same pass (the logits are dead after
+the loss, so the backward never re-reads them as logits).
+
+backward mirrors it in reverse with fp32 weight-gradient GEMMs that accumulate straight into
+the flat gradient buffer (``addmm(out_dtype=fp32, beta=1)``), LayerNorm backward kernels that
+also emit the bf16 copy of ``dx`` and the projection-bias column sums, and a flash-attention
+backward.  The loss-gradient scale (``1/grad_accum``) is folded into the first backward kernel
+through a device scalar — no host sync anywhere in the step.
+
+After each block's gradients are final the engine calls ``grad_ready(segment_name)`` so a
+data-parallel reducer (:mod:`llmtrain.parallel.reducer`) can all-reduce that bucket while the
+remaining backward runs (reference: torch DDP Reducer hooks, ``training/trainer.py:86-91``).
+
+Reference call sites replaced: ``models/gpt.py:49-74`` (attention), ``:86-105`` (LN/MLP),
+``:176-184`` (embeddings, ln_f, lm_head), ``:256-269`` (cross-entropy + masked mean).
+"""
+
+from __future__ import annotations
+
+from collections.abc import Callable
+from dataclasses import dataclass, field
+from typing import Any
+
+import torch
+
+from llmtrain import ops
+from llmtrain.runtime.flat import FlatParamStore
+
+__all__ = ["FusedGPTEngine"]
+
+VOCAB_PAD = 64  # pad the LM-head rows to a multiple of the MFMA-friendly tile
+
+
+def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    return torch.mm(a, b)
+
+
+_WGRAD_MODE: dict[str, str] = {}
+
+
+def accumulate_wgrad(dst: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
+    """``dst (fp32) += dy^T @ x`` with low-precision operands and fp32 accumulation.
+
+    Uses ``addmm(..., out_dtype=float32)`` in place (hipBLASLt with an fp32 C/D matrix) when the
+    backend supports it, else a fp32-output GEMM plus an add.
+    """
+    if dy.dtype == torch.float32:
+        dst.addmm_(dy.t(), x)
+        return
+    key = str(dst.device.type)
+    mode = _WGRAD_MODE.get(key)
+    if mode in (None, "inplace"):
+        try:
+            torch.addmm(dst, dy.t(), x, out_dtype=torch.float32, out=dst)
+            _WGRAD_MODE[key] = "inplace"
+            return
+        except (RuntimeError, TypeError):
+            if mode == "inplace":
+                raise
+            _WGRAD_MODE[key] = "mm"
+    dst.add_(torch.mm(dy.t(), x, out_dtype=torch.float32))
+
+
+@dataclass
+class _BlockActs:
+    xs: torch.Tensor  # fp32 residual stream entering the attention sub-block
+    h1: torch.Tensor
+    mu1: torch.Tensor
+    rs1: torch.Tensor
+    qkv: torch.Tensor
+    att: torch.Tensor
+    lse: torch.Tensor
+    xm: torch.Tensor  # fp32 residual stream entering the MLP sub-block
+    h2: torch.Tensor
+    mu2: torch.Tensor
+    rs2: torch.Tensor
+    u: torch.Tensor
+    g: torch.Tensor
+
+
+@dataclass
+class _StepState:
+    ids: torch.Tensor
+    bsz: int
+    seqlen: int
+    blocks: list[_BlockActs] = field(default_factory=list)
+    xf: torch.Tensor | None = None
+    hf: torch.Tensor | None = None
+    muf: torch.Tensor | None = None
+    rsf: torch.Tensor | None = None
+    dlogits: torch.Tensor | None = None
+
+
+class _FusedLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, engine, ids, labels, mask):  # type: ignore[override]
+        loss, state = engine._forward(ids, labels, mask, keep=True)
+        ctx.engine = engine
+        ctx.state = state
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_out):  # type: ignore[override]
+        state, ctx.state = ctx.state, None
+        ctx.engine._backward(state, grad_out)
+        return None, None, None, None, None
+
+
+class FusedGPTEngine:
+    """Owns the flat parameter store of a GPT and runs its fused forward/backward."""
+
+    def __init__(self, model: Any, *, compute_dtype: torch.dtype = torch.bfloat16) -> None:
+        self.model = model
+        self.compute_dtype = compute_dtype
+        self.blocks = list(model.blocks)
+        self.n_heads = model.n_heads
+        self.vocab = model.vocab_size
+        self.eps = model.ln_f.eps
+        for blk in self.blocks:
+            if blk.ln_1.eps != self.eps or blk.ln_2.eps != self.eps:
+                raise ValueError("fused engine assumes one LayerNorm eps for the whole model")
+
+        groups: list[tuple[str, list[torch.nn.Parameter]]] = [
+            ("ln_f", [model.ln_f.weight, model.ln_f.bias])
+        ]
+        for i in reversed(range(len(self.blocks))):
+            b = self.blocks[i]
+            groups.append(
+                (
+                    f"block{i}",
+                    [
+                        b.mlp_proj.weight, b.mlp_proj.bias, b.mlp_fc.weight, b.mlp_fc.bias,
+                        b.ln_2.weight, b.ln_2.bias, b.attn.out_proj.weight, b.attn.out_proj.bias,
+                        b.attn.qkv_proj.weight, b.attn.qkv_proj.bias, b.ln_1.weight, b.ln_1.bias,
+                    ],
+                )
+            )
+        emb = [model.position_embedding.weight]
+        if model.tie_embeddings:
+            emb.append(model.token_embedding.weight)
+        else:
+            emb += [model.token_embedding.weight, model.lm_head.weight]
+        groups.append(("embed", emb))
+        self.segment_order = [name for name, _ in groups]
+        self.store = FlatParamStore(groups, shadow_dtype=compute_dtype, pad_last_rows=VOCAB_PAD)
+        self.grad_ready: Callable[[str], None] | None = None
+        self.padding_seen = torch.zeros((), dtype=torch.bool, device=self.store.device)
+        self._anchor = torch.zeros((), requires_grad=True, device=self.store.device)
+
+    # ------------------------------------------------------------------------------------
+
+    @property
+    def head_weight(self) -> torch.nn.Parameter:
+        return self.model.lm_head.weight
+
+    def _w(self, p: torch.Tensor) -> torch.Tensor:
+        return self.store.shadow_of(p)
+
+    def _g(self, p: torch.Tensor) -> torch.Tensor:
+        return self.store.grad_of(p)
+
+    def _linear(self, x: torch.Tensor, layer: torch.nn.Linear) -> torch.Tensor:
+        w = self._w(layer.weight)
+        if layer.bias is None:
+            return torch.mm(x, w.t())
+        return torch.addmm(self._w(layer.bias), x, w.t())
+
+    def loss(self, ids: torch.Tensor, labels: torch.Tensor, mask: torch.Tensor | None) -> torch.Tensor:
+        self.store.sync_shadow()
+        if torch.is_grad_enabled():
+            return _FusedLoss.apply(self._anchor, self, ids, labels, mask)
+        loss, _ = self._forward(ids, labels, mask, keep=False)
+        return loss
+
+    # -- forward ---------------------------------------------------------------------------
+
+    def _forward(self, ids, labels, mask, *, keep: bool):
+        m = self.model
+        bsz, seqlen = ids.shape
+        n_tok = bsz * seqlen
+        cdt = self.compute_dtype
+        state = _StepState(ids=ids, bsz=bsz, seqlen=seqlen)
+
+        if mask is not None:
+            # The fused attention has no key-padding path: record padded batches on-device and
+            # let the trainer raise at its next sync point (no per-step host sync here).
+            self.padding_seen |= ~mask.bool().all()
+            row_w = mask.reshape(-1).float()
+            row_w = row_w / row_w.sum().clamp_min(1.0)
+        else:
+            row_w = torch.full((n_tok,), 1.0 / n_tok, dtype=torch.float32, device=ids.device)
+
+        x = ops.embedding_fwd(ids, m.token_embedding.weight, m.position_embedding.weight)
+        delta: torch.Tensor | None = None
+        for blk in self.blocks:
+            xs, h1, mu1, rs1 = ops.add_layernorm_fwd(x, delta, blk.ln_1.weight, blk.ln_1.bias, self.eps, cdt)
+            qkv = self._linear(h1, blk.attn.qkv_proj)
+            att, lse = ops.attn_fwd(qkv, bsz, seqlen, self.n_heads)
+            y = self._linear(att, blk.attn.out_proj)
+            xm, h2, mu2, rs2 = ops.add_layernorm_fwd(xs, y, blk.ln_2.weight, blk.ln_2.bias, self.eps, cdt)
+            u = self._linear(h2, blk.mlp_fc)
+            g = ops.gelu_fwd(u)
+            delta = self._linear(g, blk.mlp_proj)
+            x = xm
+            if keep:
+                state.blocks.append(_BlockActs(xs, h1, mu1, rs1, qkv, att, lse, xm, h2, mu2, rs2, u, g))
+        xf, hf, muf, rsf = ops.add_layernorm_fwd(x, delta, m.ln_f.weight, m.ln_f.bias, self.eps, cdt)
+        head = self.store.shadow_of(self.head_weight, padded=True)
+        logits = torch.mm(hf, head.t())  # [M, Vp]
+        per_row = ops.cross_entropy_fwd_bwd(logits, labels.reshape(-1), self.vocab, row_w)
+        loss = torch.dot(per_row, row_w)
+        if keep:
+            state.xf, state.hf, state.muf, state.rsf = xf, hf, muf, rsf
+            state.dlogits = logits
+        return loss, state
+
+    # -- backward --------------------------------------------------------------------------
+
+    def _notify(self, segment: str) -> None:
+        if self.grad_ready is not None:
+            self.grad_ready(segment)
+
+    def _backward(self, st: _StepState, grad_out: torch.Tensor) -> None:
+        m = self.model
+        bsz, seqlen = st.bsz, st.seqlen
+        go = grad_out.detach().reshape(()).float()
+        dlogits = st.dlogits
+        assert dlogits is not None and st.hf is not None
+        head = self.store.shadow_of(self.head_weight, padded=True)
+
+        # LM head: dhf = dlogits @ W ; dW += dlogits^T @ (go * hf)
+        dhf = torch.mm(dlogits, head)
+        hf_scaled = (st.hf.float() * go).to(st.hf.dtype) if st.hf.dtype != torch.float32 else st.hf * go
+        accumulate_wgrad(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled)
+        del hf_scaled
+        st.dlogits = None
+        del dlogits
+
+        last = self.blocks[-1]
+        dx, dx_lp = ops.layernorm_bwd(
+            dhf, st.xf, st.muf, st.rsf, m.ln_f.weight, None, self._g(m.ln_f.weight), self._g(m.ln_f.bias),
+            go, want_lowp=True, dproj_bias=self._g(last.mlp_proj.bias),
+        )
+        del dhf
+        self._notify("ln_f")
+
+        for i in reversed(range(len(self.blocks))):
+            blk, a = self.blocks[i], st.blocks[i]
+            # MLP: delta = g Wp^T + bp ; dx is d(delta) (bias grad already summed by the LN bwd)
+            accumulate_wgrad(self._g(blk.mlp_proj.weight), dx_lp, a.g)
+            dg = torch.mm(dx_lp, self._w(blk.mlp_proj.weight))
+            du = ops.gelu_bwd(dg, a.u, self._g(blk.mlp_fc.bias))
+            del dg
+            accumulate_wgrad(self._g(blk.mlp_fc.weight), du, a.h2)
+            dh2 = torch.mm(du, self._w(blk.mlp_fc.weight))
+            del du
+            dxm, dy_lp = ops.layernorm_bwd(
+                dh2, a.xm, a.mu2, a.rs2, blk.ln_2.weight, dx, self._g(blk.ln_2.weight), self._g(blk.ln_2.bias),
+                None, want_lowp=True, dproj_bias=self._g(blk.attn.out_proj.bias),
+            )
+            del dh2, dx, dx_lp
+            # attention output projection
+            accumulate_wgrad(self._g(blk.attn.out_proj.weight), dy_lp, a.att)
+            datt = torch.mm(dy_lp, self._w(blk.attn.out_proj.weight))
+            del dy_lp
+            dqkv = ops.attn_bwd(datt, a.qkv, a.att, a.lse, bsz, seqlen, self.n_heads)
+            del datt
+            ops.colsum_accum(dqkv, self._g(blk.attn.qkv_proj.bias))
+            accumulate_wgrad(self._g(blk.attn.qkv_proj.weight), dqkv, a.h1)
+            dh1 = torch.mm(dqkv, self._w(blk.attn.qkv_proj.weight))
+            del dqkv
+            prev_bias = self._g(self.blocks[i - 1].mlp_proj.bias) if i > 0 else None
+            dx, dx_lp = ops.layernorm_bwd(
+                dh1, a.xs, a.mu1, a.rs1, blk.ln_1.weight, dxm, self._g(blk.ln_1.weight), self._g(blk.ln_1.bias),
+                None, want_lowp=i > 0, dproj_bias=prev_bias,
+            )
+            del dh1, dxm
+            st.blocks[i] = None  # type: ignore[call-overload]  # free activations early
+            self._notify(f"block{i}")
+
+        ops.embedding_bwd(dx, st.ids, self._g(m.token_embedding.weight), self._g(m.position_embedding.weight))
+        self._notify("embed")

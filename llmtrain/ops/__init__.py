@@ -1,0 +1,136 @@
+"""Fused ops of the MI355X training path.
+
+Each function runs the hand-written gfx950 HIP kernel (``torch.ops.llmtrain_hip.*``) when its
+inputs live on a GPU and the plain-PyTorch oracle from :mod:`llmtrain.ops.reference` when they
+live on the CPU (unit tests of the fused engine).  There is exactly one GPU implementation per
+op and no silent fallback: a GPU tensor with the extension missing raises (``_ext.require``).
+"""
+
+from __future__ import annotations
+
+import torch
+
+from llmtrain.ops import _ext
+from llmtrain.ops import reference as ref
+
+__all__ = [
+    "adamw_flat",
+    "add_layernorm_fwd",
+    "attn_bwd",
+    "attn_fwd",
+    "colsum_accum",
+    "cross_entropy_fwd_bwd",
+    "embedding_bwd",
+    "embedding_fwd",
+    "gelu_bwd",
+    "gelu_fwd",
+    "hip_ops",
+    "layernorm_bwd",
+    "sumsq",
+]
+
+
+def hip_ops():  # noqa: ANN201 - torch op namespace
+    _ext.require()
+    return torch.ops.llmtrain_hip
+
+
+def _on_gpu(t: torch.Tensor) -> bool:
+    return t.device.type == "cuda"
+
+
+def add_layernorm_fwd(x, delta, weight, bias, eps: float, out_dtype: torch.dtype):
+    if _on_gpu(x):
+        xs, y, mean, rstd = hip_ops().add_layernorm_fwd(x, delta, weight, bias, eps, out_dtype)
+        return (x if delta is None else xs), y, mean, rstd
+    return ref.add_layernorm_fwd(x, delta, weight, bias, eps, out_dtype)
+
+
+def layernorm_bwd(
+    dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale=None, *, want_lowp=False, dproj_bias=None
+):
+    """LayerNorm backward with two optional fusions for the producer of the normalised input:
+
+    * ``want_lowp`` also returns ``dx`` in ``dy``'s dtype (the GEMM operand of the projection
+      whose output was added to the residual stream), and
+    * ``dproj_bias`` (fp32 ``[d]``) accumulates ``colsum(dx)`` — that projection's bias grad.
+
+    Returns ``(dx_fp32, dx_lowp | None)``.
+    """
+    if _on_gpu(dy):
+        dx, dx_lp = hip_ops().layernorm_bwd(
+            dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale, want_lowp, dproj_bias
+        )
+        return dx, (dx_lp if want_lowp else None)
+    dx = ref.layernorm_bwd(dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale)
+    if dproj_bias is not None:
+        ref.colsum_accum(dx, dproj_bias)
+    return dx, (dx.to(dy.dtype) if want_lowp else None)
+
+
+def cross_entropy_fwd_bwd(logits, labels, vocab: int, row_weight):
+    if _on_gpu(logits):
+        return hip_ops().cross_entropy_fwd_bwd(logits, labels, vocab, row_weight)
+    return ref.cross_entropy_fwd_bwd(logits, labels, vocab, row_weight)
+
+
+def gelu_fwd(u):
+    if _on_gpu(u):
+        return hip_ops().gelu_fwd(u)
+    return ref.gelu_fwd(u)
+
+
+def gelu_bwd(dg, u, dbias):
+    if _on_gpu(dg):
+        return hip_ops().gelu_bwd(dg, u, dbias)
+    return ref.gelu_bwd(dg, u, dbias)
+
+
+def colsum_accum(dy, out) -> None:
+    if _on_gpu(dy):
+        hip_ops().colsum_accum(dy, out)
+    else:
+        ref.colsum_accum(dy, out)
+
+
+def embedding_fwd(ids, wte, wpe):
+    if _on_gpu(ids):
+        return hip_ops().embedding_fwd(ids, wte, wpe)
+    return ref.embedding_fwd(ids, wte, wpe)
+
+
+def embedding_bwd(dx, ids, dwte, dwpe) -> None:
+    if _on_gpu(dx):
+        hip_ops().embedding_bwd(dx, ids, dwte, dwpe)
+    else:
+        ref.embedding_bwd(dx, ids, dwte, dwpe)
+
+
+def attn_fwd(qkv, bsz: int, seqlen: int, n_heads: int):
+    if _on_gpu(qkv):
+        return hip_ops().attn_fwd(qkv, bsz, seqlen, n_heads)
+    return ref.attn_fwd(qkv, bsz, seqlen, n_heads)
+
+
+def attn_bwd(dout, qkv, out, lse, bsz: int, seqlen: int, n_heads: int):
+    if _on_gpu(dout):
+        return hip_ops().attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads)
+    return ref.attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads)
+
+
+def sumsq(x):
+    if _on_gpu(x):
+        return hip_ops().sumsq(x)
+    return ref.sumsq(x)
+
+
+def adamw_flat(param, grad, exp_avg, exp_avg_sq, shadow, *, lr, beta1, beta2, eps, weight_decay, step, grad_scale):
+    if _on_gpu(param):
+        hip_ops().adamw_flat(
+            param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps, weight_decay, step, grad_scale
+        )
+        return
+    ref.adamw_flat(
+        param, grad, exp_avg, exp_avg_sq, shadow, lr=lr, beta1=beta1, beta2=beta2, eps=eps,
+        weight_decay=weight_decay, step=step, grad_scale=grad_scale,
+    )

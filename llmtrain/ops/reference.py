@@ -1,0 +1,238 @@
+"""Plain-PyTorch fp32 reference implementations of every fused op.
+
+These are the numerics oracles for the HIP kernels (``tests/test_kernels_gpu.py`` compares each
+kernel against the function of the same name here) and the implementation used when the fused
+GPT engine runs on CPU (unit tests of the hand-written backward).  Signatures mirror the HIP
+ops in ``csrc/bindings.cpp`` exactly, including in-place accumulation into gradient buffers.
+
+Layout conventions shared with the kernels:
+* activations are row-major ``[M, C]`` with ``M = B*T`` tokens;
+* ``qkv`` is the packed projection output ``[B, T, 3, H, Dh]`` (viewed as ``[B*T, 3*d]``);
+* attention ``lse`` is the natural-log softmax normaliser per (b, h, t), ``[B, H, T]`` fp32;
+* weight/bias gradient buffers are fp32 and are *accumulated into* (never overwritten).
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+__all__ = [
+    "adamw_flat",
+    "add_layernorm_fwd",
+    "attn_bwd",
+    "attn_fwd",
+    "colsum_accum",
+    "cross_entropy_fwd_bwd",
+    "embedding_bwd",
+    "embedding_fwd",
+    "gelu_bwd",
+    "gelu_fwd",
+    "layernorm_bwd",
+    "sumsq",
+]
+
+_INV_SQRT2 = 1.0 / math.sqrt(2.0)
+_INV_SQRT_2PI = 1.0 / math.sqrt(2.0 * math.pi)
+
+
+def add_layernorm_fwd(
+    x: torch.Tensor,
+    delta: torch.Tensor | None,
+    weight: torch.Tensor,
+    bias: torch.Tensor,
+    eps: float,
+    out_dtype: torch.dtype,
+) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """``xs = x + delta`` (fp32 residual update), ``y = LN(xs)`` cast to ``out_dtype``.
+
+    Returns ``(xs, y, mean, rstd)``; when ``delta`` is None ``xs`` is ``x`` itself.
+    """
+    xs = x if delta is None else x + delta.float()
+    mean = xs.mean(dim=-1)
+    var = (xs - mean[:, None]).pow(2).mean(dim=-1)
+    rstd = torch.rsqrt(var + eps)
+    y = (xs - mean[:, None]) * rstd[:, None] * weight.float() + bias.float()
+    return xs, y.to(out_dtype), mean, rstd
+
+
+def layernorm_bwd(
+    dy: torch.Tensor,
+    xs: torch.Tensor,
+    mean: torch.Tensor,
+    rstd: torch.Tensor,
+    weight: torch.Tensor,
+    dresid: torch.Tensor | None,
+    dweight: torch.Tensor,
+    dbias: torch.Tensor,
+    dy_scale: torch.Tensor | None = None,
+) -> torch.Tensor:
+    """LayerNorm backward. Returns ``dx`` (fp32) = ``dresid + dLN/dx``; accumulates dγ, dβ.
+
+    ``dy_scale`` (0-d fp32 tensor) multiplies ``dy`` first (used to fold the loss gradient
+    scale into the first backward kernel without a host sync).
+    """
+    g = dy.float()
+    if dy_scale is not None:
+        g = g * dy_scale.float()
+    xhat = (xs - mean[:, None]) * rstd[:, None]
+    dweight += (g * xhat).sum(dim=0)
+    dbias += g.sum(dim=0)
+    gw = g * weight.float()
+    dx = rstd[:, None] * (gw - gw.mean(dim=-1, keepdim=True) - xhat * (gw * xhat).mean(dim=-1, keepdim=True))
+    if dresid is not None:
+        dx = dx + dresid
+    return dx
+
+
+def cross_entropy_fwd_bwd(
+    logits: torch.Tensor, labels: torch.Tensor, vocab: int, row_weight: torch.Tensor
+) -> torch.Tensor:
+    """Per-row CE loss over the first ``vocab`` columns; overwrites ``logits`` with dlogits.
+
+    ``logits`` ``[M, Vp]`` (``Vp >= vocab``, padded columns ignored and given zero gradient),
+    ``labels`` ``[M]`` int64 (negative = ignored row: loss 0, gradient 0), ``row_weight`` ``[M]``
+    fp32 — the gradient of row ``i`` is ``(softmax - onehot) * row_weight[i]``.
+    Returns the unweighted per-row loss ``[M]`` fp32.
+    """
+    z = logits[:, :vocab].float()
+    lse = torch.logsumexp(z, dim=-1)
+    valid = labels >= 0
+    safe = torch.where(valid, labels, torch.zeros_like(labels))
+    picked = z.gather(1, safe[:, None]).squeeze(1)
+    loss = torch.where(valid, lse - picked, torch.zeros_like(lse))
+    grad = torch.softmax(z, dim=-1)
+    grad[torch.arange(z.shape[0], device=z.device), safe] -= 1.0
+    grad = grad * (row_weight * valid.float())[:, None]
+    logits[:, :vocab] = grad.to(logits.dtype)
+    if logits.shape[1] > vocab:
+        logits[:, vocab:] = 0
+    return loss
+
+
+def gelu_fwd(u: torch.Tensor) -> torch.Tensor:
+    """Exact (erf) GELU, same dtype as the input (``nn.GELU()`` default, reference gpt.py:95)."""
+    return F.gelu(u.float()).to(u.dtype)
+
+
+def gelu_bwd(dg: torch.Tensor, u: torch.Tensor, dbias: torch.Tensor | None) -> torch.Tensor:
+    """``du = dg * gelu'(u)`` in ``u.dtype``; accumulates ``colsum(du)`` into ``dbias``."""
+    uf = u.float()
+    cdf = 0.5 * (1.0 + torch.erf(uf * _INV_SQRT2))
+    pdf = torch.exp(-0.5 * uf * uf) * _INV_SQRT_2PI
+    du = dg.float() * (cdf + uf * pdf)
+    if dbias is not None:
+        dbias += du.sum(dim=0)
+    return du.to(u.dtype)
+
+
+def colsum_accum(dy: torch.Tensor, out: torch.Tensor) -> None:
+    """``out += dy.sum(0)`` in fp32 (bias gradients)."""
+    out += dy.float().sum(dim=0)
+
+
+def embedding_fwd(ids: torch.Tensor, wte: torch.Tensor, wpe: torch.Tensor) -> torch.Tensor:
+    """``x[b*T+t] = wte[ids[b,t]] + wpe[t]`` → ``[B*T, d]`` fp32."""
+    bsz, seqlen = ids.shape
+    x = wte.float()[ids.reshape(-1)] + wpe.float()[:seqlen].repeat(bsz, 1)
+    return x
+
+
+def embedding_bwd(
+    dx: torch.Tensor, ids: torch.Tensor, dwte: torch.Tensor, dwpe: torch.Tensor
+) -> None:
+    """Scatter-add token gradients into ``dwte``; sum over the batch into ``dwpe[:T]``."""
+    bsz, seqlen = ids.shape
+    dwte.index_add_(0, ids.reshape(-1), dx.float())
+    dwpe[:seqlen] += dx.float().view(bsz, seqlen, -1).sum(dim=0)
+
+
+def _split_qkv(qkv: torch.Tensor, bsz: int, seqlen: int, n_heads: int):
+    d = qkv.shape[-1] // 3
+    q, k, v = qkv.view(bsz, seqlen, 3, n_heads, d // n_heads).unbind(dim=2)
+    return q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+
+
+def attn_fwd(qkv: torch.Tensor, bsz: int, seqlen: int, n_heads: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """Causal attention over packed ``qkv`` ``[B*T, 3d]``.
+
+    Returns ``out`` ``[B*T, d]`` (dtype of qkv) and ``lse`` ``[B, H, T]`` fp32.
+    """
+    q, k, v = (t.float() for t in _split_qkv(qkv, bsz, seqlen, n_heads))
+    hd = q.shape[-1]
+    s = (q @ k.transpose(-2, -1)) / math.sqrt(hd)
+    causal = torch.ones(seqlen, seqlen, dtype=torch.bool, device=qkv.device).triu(1)
+    s = s.masked_fill(causal, float("-inf"))
+    lse = torch.logsumexp(s, dim=-1)
+    p = torch.exp(s - lse[..., None])
+    out = (p @ v).transpose(1, 2).reshape(bsz * seqlen, n_heads * hd)
+    return out.to(qkv.dtype), lse
+
+
+def attn_bwd(
+    dout: torch.Tensor,
+    qkv: torch.Tensor,
+    out: torch.Tensor,
+    lse: torch.Tensor,
+    bsz: int,
+    seqlen: int,
+    n_heads: int,
+) -> torch.Tensor:
+    """Gradient of :func:`attn_fwd` w.r.t. packed ``qkv``; returns ``[B*T, 3d]`` in qkv dtype."""
+    q, k, v = (t.float() for t in _split_qkv(qkv, bsz, seqlen, n_heads))
+    hd = q.shape[-1]
+    scale = 1.0 / math.sqrt(hd)
+    do = dout.float().view(bsz, seqlen, n_heads, hd).transpose(1, 2)
+    o = out.float().view(bsz, seqlen, n_heads, hd).transpose(1, 2)
+    s = (q @ k.transpose(-2, -1)) * scale
+    causal = torch.ones(seqlen, seqlen, dtype=torch.bool, device=qkv.device).triu(1)
+    p = torch.exp(s - lse[..., None]).masked_fill(causal, 0.0)
+    dv = p.transpose(-2, -1) @ do
+    dp = do @ v.transpose(-2, -1)
+    delta = (do * o).sum(dim=-1, keepdim=True)
+    ds = p * (dp - delta) * scale
+    dq = ds @ k
+    dk = ds.transpose(-2, -1) @ q
+    dqkv = torch.stack([dq, dk, dv], dim=2)  # [B, H, 3, T, hd]
+    dqkv = dqkv.permute(0, 3, 2, 1, 4).reshape(bsz * seqlen, 3 * n_heads * hd)
+    return dqkv.to(qkv.dtype)
+
+
+def sumsq(x: torch.Tensor) -> torch.Tensor:
+    """Σ x² in fp32 as a 0-d tensor."""
+    return x.float().pow(2).sum()
+
+
+def adamw_flat(
+    param: torch.Tensor,
+    grad: torch.Tensor,
+    exp_avg: torch.Tensor,
+    exp_avg_sq: torch.Tensor,
+    shadow: torch.Tensor | None,
+    *,
+    lr: float,
+    beta1: float,
+    beta2: float,
+    eps: float,
+    weight_decay: float,
+    step: int,
+    grad_scale: torch.Tensor | None,
+) -> None:
+    """One decoupled-weight-decay Adam step over flat fp32 buffers (torch.optim.AdamW math).
+
+    ``grad_scale`` (0-d fp32) multiplies the gradient first (gradient clipping without a host
+    sync). When ``shadow`` is given, the updated parameters are also written to it (bf16 copy
+    used by the compute path); ``shadow`` may be longer than ``param`` (padding is untouched).
+    """
+    g = grad if grad_scale is None else grad * grad_scale
+    param.mul_(1.0 - lr * weight_decay)
+    exp_avg.lerp_(g, 1.0 - beta1)
+    exp_avg_sq.mul_(beta2).addcmul_(g, g, value=1.0 - beta2)
+    bc1 = 1.0 - beta1**step
+    bc2 = 1.0 - beta2**step
+    denom = (exp_avg_sq.sqrt() / math.sqrt(bc2)).add_(eps)
+    param.addcdiv_(exp_avg, denom, value=-lr / bc1)
+    if shadow is not None:
+        shadow[: param.numel()].copy_(param)

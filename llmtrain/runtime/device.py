@@ -1,0 +1,66 @@
+"""Device, precision and seeding policy — decided once per run and passed down.
+
+* ``run.device``: ``cpu`` | ``mps`` | ``cuda``/``rocm`` → ``cuda:<local_rank>`` (HIP GPU).
+* ``run.precision``: ``fp32`` (reference numerics) | ``bf16`` (MI355X compute path).
+* ``run.seed`` seeds python/numpy/torch (+ all HIP devices) BEFORE the model is built — the
+  reference validates but never applies the seed; applying it here is an
+  intentional, documented fix so runs are reproducible and ranks initialise identically.
+"""
+
+from __future__ import annotations
+
+import random
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from llmtrain.config.schemas import RunConfig
+
+__all__ = ["RuntimePolicy", "resolve_policy", "seed_everything"]
+
+
+@dataclass(frozen=True)
+class RuntimePolicy:
+    device: torch.device
+    compute_dtype: torch.dtype
+    use_fused: bool
+
+    @property
+    def is_gpu(self) -> bool:
+        return self.device.type == "cuda"
+
+    def autocast(self):  # type: ignore[no-untyped-def]
+        """Autocast context for the module path (no-op for fp32 or the fused engine)."""
+        import contextlib
+
+        if self.is_gpu and self.compute_dtype == torch.bfloat16 and not self.use_fused:
+            return torch.autocast(device_type="cuda", dtype=torch.bfloat16)
+        return contextlib.nullcontext()
+
+
+def _device_for(cfg: RunConfig, local_rank: int) -> torch.device:
+    if cfg.run.device in ("cuda", "rocm"):
+        if not torch.cuda.is_available():
+            raise RuntimeError("run.device requests a GPU but no HIP device is visible")
+        return torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+    return torch.device(cfg.run.device)
+
+
+def resolve_policy(cfg: RunConfig, *, local_rank: int = 0, fused_capable: bool = False) -> RuntimePolicy:
+    device = _device_for(cfg, local_rank)
+    compute = torch.bfloat16 if cfg.run.precision == "bf16" else torch.float32
+    setting = cfg.model.extra.get("fused", "auto")
+    if setting == "auto":
+        use_fused = fused_capable and device.type == "cuda" and compute == torch.bfloat16
+    else:
+        use_fused = bool(setting) and fused_capable
+    return RuntimePolicy(device=device, compute_dtype=compute, use_fused=use_fused)
+
+
+def seed_everything(seed: int) -> None:
+    random.seed(seed)
+    np.random.seed(seed % 2**32)
+    torch.manual_seed(seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed_all(seed)

@@ -1,0 +1,541 @@
+"""Optimizer-step training loop (reference ``training/trainer.py:30-548``), MI355X build.
+
+Loop semantics kept from the reference: ``grad_accum_steps`` micro-batches per optimizer step
+(communication skipped on all but the last), global-norm clipping, AdamW, a LambdaLR with
+linear warm-up then cosine decay to 0 at ``max_steps`` (step 0 uses lr=0 when warm-up > 0),
+rank-0 checkpointing BEFORE evaluation, interval metrics every ``log_every_steps`` and at the
+final step, token-weighted evaluation every ``eval_every_steps`` and at the final step, and
+``--resume`` from a run id, checkpoint directory or ``step_N.pt``.
+
+What changes on the MI355X path:
+
+* the fused GPT engine + flat-buffer gradient reducer + fused AdamW (one kernel, clip
+  coefficient read on device) replace autograd/DDP/foreach-AdamW when the model supports it;
+* the loss is accumulated ON DEVICE; the host reads it once per log interval (the reference
+  calls ``.item()`` on every micro-step — a pipeline-draining sync);
+* metric collectives use device tensors (RCCL cannot reduce CPU tensors);
+* resume replays the data order on every rank (each rank skips its own shard's batches — the
+  reference disables replay under DDP);
+* ``peak_memory`` reports ``torch.cuda.max_memory_allocated`` (GiB) on GPU;
+* optional ``trainer.extra``: ``keep_last_k``, ``fail_at_step`` (fault injection),
+  ``profile`` (torch.profiler window), ``bucket_cap_mb``, ``grad_reduce_dtype``.
+"""
+
+from __future__ import annotations
+
+import contextlib
+import logging
+import math
+import time
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Any
+
+import torch
+import torch.distributed as dist
+from torch import nn
+
+from llmtrain.config.schemas import RunConfig
+from llmtrain.parallel.ddp import unwrap, wrap_data_parallel
+from llmtrain.parallel.dist import DDPState
+from llmtrain.registry import initialize_registries
+from llmtrain.registry.data import get_data_module
+from llmtrain.registry.models import get_model_adapter
+from llmtrain.runtime.device import resolve_policy, seed_everything
+from llmtrain.tracking import NullTracker, Tracker
+from llmtrain.training.checkpoint import CheckpointManager, CheckpointPayload, restore_rng_states
+from llmtrain.training.optim import FusedAdamW, build_optimizer, fused_clip_coef
+
+__all__ = ["TrainResult", "Trainer", "lr_lambda_factory"]
+
+logger = logging.getLogger(__name__)
+
+
+@dataclass(frozen=True)
+class TrainResult:
+    final_step: int
+    final_loss: float
+    final_val_loss: float | None
+    total_time: float
+    peak_memory: float
+    val_metrics: dict[str, float] | None = None
+    first_step_loss: float | None = None
+    resumed_from_step: int | None = None
+    parameter_count: int | None = None
+    trainable_parameter_count: int | None = None
+
+
+def lr_lambda_factory(warmup_steps: int, max_steps: int):  # type: ignore[no-untyped-def]
+    """Linear warm-up 0→1 over ``warmup_steps``, then cosine 1→0 reaching 0 at ``max_steps``."""
+
+    def lr_lambda(step: int) -> float:
+        if step < warmup_steps:
+            return step / warmup_steps
+        if step >= max_steps:
+            return 0.0
+        if max_steps <= warmup_steps:
+            return 1.0
+        progress = (step - warmup_steps) / (max_steps - warmup_steps)
+        return 0.5 * (1.0 + math.cos(math.pi * progress))
+
+    return lr_lambda
+
+
+def _to_device(batch: dict[str, Any], device: torch.device) -> dict[str, Any]:
+    non_blocking = device.type == "cuda"
+    return {
+        k: v.to(device, non_blocking=non_blocking) if torch.is_tensor(v) else v for k, v in batch.items()
+    }
+
+
+def _loss_tensor(loss: torch.Tensor, metrics: dict[str, Any]) -> torch.Tensor:
+    value = metrics.get("loss")
+    tensor = getattr(value, "tensor", None)
+    if isinstance(tensor, torch.Tensor):
+        return tensor.detach().float()
+    if value is not None and not isinstance(value, torch.Tensor):
+        return torch.tensor(float(value), dtype=torch.float32, device=loss.device)
+    return loss.detach().float()
+
+
+class _Batches:
+    """Endless iterator over a DataLoader that restarts it at each epoch boundary."""
+
+    def __init__(self, loader: Any) -> None:
+        self._loader = loader
+        self._it = iter(loader)
+        self.consumed = 0
+
+    def next(self) -> dict[str, Any]:
+        try:
+            batch = next(self._it)
+        except StopIteration:
+            self._it = iter(self._loader)
+            batch = next(self._it)
+        self.consumed += 1
+        return batch
+
+
+class Trainer:
+    def __init__(
+        self,
+        cfg: RunConfig,
+        *,
+        run_dir: Path | None = None,
+        tracker: Tracker | None = None,
+        ddp_state: DDPState | None = None,
+    ) -> None:
+        self._cfg = cfg
+        self._tracker: Tracker = tracker or NullTracker()
+        self._ddp_state = ddp_state
+        initialize_registries()
+        seed_everything(cfg.run.seed)
+
+        self._adapter = get_model_adapter(cfg.model.name)()
+        data_module = get_data_module(cfg.data.name)()
+        model = self._adapter.build_model(cfg)
+        tokenizer = self._adapter.build_tokenizer(cfg)
+        data_module.setup(cfg, tokenizer=tokenizer)
+        self._train_loader = data_module.train_dataloader()
+        self._val_loader = data_module.val_dataloader()
+
+        local_rank = ddp_state.local_rank if ddp_state is not None else 0
+        fused_capable = hasattr(model, "prepare_runtime") and bool(
+            getattr(model, "fused_supported", lambda: False)()
+        )
+        self._policy = resolve_policy(cfg, local_rank=local_rank, fused_capable=fused_capable)
+        self._device = self._policy.device
+        model = model.to(self._device)
+        if self._policy.use_fused:
+            model.prepare_runtime(compute_dtype=self._policy.compute_dtype)
+        self._model: nn.Module = model
+        if self._is_ddp_active:
+            self._model = wrap_data_parallel(model, cfg, self._device)
+
+        self._optimizer = build_optimizer(unwrap(self._model), cfg.trainer.lr, cfg.trainer.weight_decay)
+        self._scheduler = self._build_scheduler(self._optimizer)
+        self._ckpt_mgr: CheckpointManager | None = None
+        if run_dir is not None:
+            keep = int(cfg.trainer.extra.get("keep_last_k", 3))
+            self._ckpt_mgr = CheckpointManager(run_dir / "checkpoints", keep_last_k=keep)
+        self._run_dir = run_dir
+        logger.info(
+            "trainer: device=%s compute_dtype=%s fused=%s ddp=%s",
+            self._device, self._policy.compute_dtype, self._policy.use_fused, self._is_ddp_active,
+        )
+
+    # -- properties ------------------------------------------------------------------------
+
+    def _build_scheduler(self, optimizer: torch.optim.Optimizer) -> torch.optim.lr_scheduler.LambdaLR:
+        fn = lr_lambda_factory(self._cfg.trainer.warmup_steps, self._cfg.trainer.max_steps)
+        return torch.optim.lr_scheduler.LambdaLR(optimizer, lr_lambda=fn)
+
+    @property
+    def scheduler(self) -> torch.optim.lr_scheduler.LambdaLR:
+        return self._scheduler
+
+    @property
+    def optimizer(self) -> torch.optim.Optimizer:
+        return self._optimizer
+
+    @property
+    def model(self) -> nn.Module:
+        return self._model
+
+    @property
+    def device(self) -> torch.device:
+        return self._device
+
+    @property
+    def _is_main(self) -> bool:
+        return self._ddp_state is None or self._ddp_state.is_main
+
+    @property
+    def _raw_model(self) -> nn.Module:
+        return unwrap(self._model)
+
+    @property
+    def _rank(self) -> int:
+        return self._ddp_state.rank if self._ddp_state is not None else 0
+
+    @property
+    def _world_size(self) -> int:
+        return self._ddp_state.world_size if self._ddp_state is not None else 1
+
+    @property
+    def _is_ddp_active(self) -> bool:
+        return self._ddp_state is not None and self._ddp_state.world_size > 1
+
+    def _metric_device(self) -> torch.device:
+        if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+            return self._device
+        return torch.device("cpu")
+
+    # -- metric collectives (C4-C7) ------------------------------------------------------------
+
+    def _reduce_metrics(self, **scalars: float) -> dict[str, float]:
+        if not self._is_ddp_active:
+            return dict(scalars)
+        keys = list(scalars)
+        t = torch.tensor([scalars[k] for k in keys], dtype=torch.float64, device=self._metric_device())
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return {k: float(v) for k, v in zip(keys, t.tolist())}
+
+    def _gather_scalars(self, **scalars: float) -> list[dict[str, float]] | None:
+        if not self._is_ddp_active:
+            return [dict(scalars)]
+        if not (dist.is_available() and dist.is_initialized()):
+            return [dict(scalars)] if self._is_main else None
+        keys = list(scalars)
+        local = torch.tensor([scalars[k] for k in keys], dtype=torch.float64, device=self._metric_device())
+        bucket = [torch.zeros_like(local) for _ in range(self._world_size)]
+        dist.all_gather(bucket, local)
+        if not self._is_main:
+            return None
+        return [{k: float(v) for k, v in zip(keys, t.tolist())} for t in bucket]
+
+    # -- resume ------------------------------------------------------------------------------
+
+    def restore(self, payload: CheckpointPayload) -> int:
+        self._raw_model.load_state_dict(payload["model_state_dict"])
+        self._optimizer.load_state_dict(payload["optimizer_state_dict"])
+        self._scheduler.load_state_dict(payload["scheduler_state_dict"])
+        restore_rng_states(payload["rng_states"])
+        store = getattr(self._raw_model, "flat_store", None)
+        if store is not None:
+            store.sync_shadow(force=True)
+        step = int(payload["step"])
+        logger.info("trainer: restored state from step %d", step)
+        return step
+
+    def _resolve_resume_path(self, resume_from: str | Path) -> Path:
+        candidate = Path(resume_from)
+        if candidate.exists():
+            if candidate.is_file():
+                return candidate
+            if candidate.is_dir():
+                latest = CheckpointManager(candidate, keep_last_k=1).latest_checkpoint()
+                if latest is None:
+                    raise FileNotFoundError(f"No checkpoints found in {candidate}")
+                return latest
+            raise FileNotFoundError(f"Resume path {candidate} is not a file or directory")
+        if candidate.suffix == ".pt":
+            raise FileNotFoundError(f"Checkpoint file {candidate} does not exist")
+        ckpt_dir = Path(self._cfg.output.root_dir) / str(resume_from) / "checkpoints"
+        if not ckpt_dir.exists():
+            raise FileNotFoundError(f"Checkpoint directory {ckpt_dir} does not exist")
+        latest = CheckpointManager(ckpt_dir, keep_last_k=1).latest_checkpoint()
+        if latest is None:
+            raise FileNotFoundError(f"No checkpoints found in {ckpt_dir}")
+        return latest
+
+    # -- evaluation ----------------------------------------------------------------------------
+
+    def _evaluate(self) -> tuple[dict[str, float], dict[str, float]] | None:
+        if self._val_loader is None:
+            return None
+        was_training = self._model.training
+        self._model.eval()
+        loss_sum = torch.zeros((), dtype=torch.float64, device=self._device)
+        tokens = 0
+        with torch.no_grad(), self._policy.autocast():
+            for batch in self._val_loader:
+                batch = _to_device(batch, self._device)
+                loss, metrics = self._adapter.compute_loss(self._raw_model, batch)
+                n = batch["input_ids"].numel()
+                loss_sum += _loss_tensor(loss, metrics).double() * n
+                tokens += n
+        if was_training:
+            self._model.train()
+        if tokens == 0:
+            return {}, {}
+        local_sum = float(loss_sum.item())
+        local = {"val/loss": local_sum / tokens}
+        if not self._is_ddp_active:
+            return local, dict(local)
+        red = self._reduce_metrics(loss_sum=local_sum, tok_count=float(tokens))
+        glob = {"val/loss": red["loss_sum"] / red["tok_count"] if red["tok_count"] > 0 else 0.0}
+        return local, glob
+
+    # -- the loop ------------------------------------------------------------------------------
+
+    def _sync_context(self, is_last_micro: bool) -> contextlib.AbstractContextManager[Any]:
+        if not is_last_micro and hasattr(self._model, "no_sync"):
+            return self._model.no_sync()
+        return contextlib.nullcontext()
+
+    def _optimizer_step(self) -> None:
+        finish = getattr(self._model, "finish_gradient_sync", None)
+        if finish is not None:
+            finish()
+        max_norm = self._cfg.trainer.max_grad_norm
+        if isinstance(self._optimizer, FusedAdamW):
+            _, coef = fused_clip_coef(self._optimizer.store, max_norm)
+            self._optimizer.step(grad_scale=coef)
+        else:
+            torch.nn.utils.clip_grad_norm_(self._model.parameters(), max_norm)
+            self._optimizer.step()
+        self._scheduler.step()
+
+    def _check_engine_flags(self) -> None:
+        engine = getattr(self._raw_model, "engine", None)
+        if engine is not None and bool(engine.padding_seen.item()):
+            raise RuntimeError(
+                "fused GPT engine received a batch with attention_mask zeros; key-padding is not "
+                "implemented on the fused path (set model.extra.fused=false)"
+            )
+
+    def _profiler(self) -> Any:
+        spec = self._cfg.trainer.extra.get("profile")
+        if not spec or self._run_dir is None or not self._is_main:
+            return None
+        from llmtrain.utils.profiling import StepProfiler
+
+        return StepProfiler(spec, self._run_dir / "profile")
+
+    def fit(
+        self,
+        *,
+        max_steps_override: int | None = None,
+        resume_from: str | Path | None = None,
+    ) -> TrainResult:
+        cfg = self._cfg.trainer
+        self._model.train()
+        max_steps = max_steps_override if max_steps_override is not None else cfg.max_steps
+        accum = cfg.grad_accum_steps
+        fail_at = self._cfg.trainer.extra.get("fail_at_step")
+        if self._device.type == "cuda":
+            torch.cuda.reset_peak_memory_stats(self._device)
+
+        batches = _Batches(self._train_loader)
+        start_step = 1
+        resumed_from_step: int | None = None
+        if resume_from is not None:
+            path = self._resolve_resume_path(resume_from)
+            payload = CheckpointManager(path.parent, keep_last_k=1).load(path)
+            if payload["config"] != self._cfg.model_dump():
+                logger.warning("checkpoint: config mismatch detected; using current config for resume")
+            resumed_from_step = self.restore(payload)
+            start_step = resumed_from_step + 1
+            if start_step > max_steps:
+                logger.info(
+                    "trainer: resume step %d >= max_steps %d; no further steps", resumed_from_step, max_steps
+                )
+        if self._is_main:
+            self._tracker.log_params(self._cfg.model_dump())
+        n_params = sum(p.numel() for p in self._raw_model.parameters())
+        n_trainable = sum(p.numel() for p in self._raw_model.parameters() if p.requires_grad)
+
+        t_start = time.perf_counter()
+        if resumed_from_step:
+            # Replay the data order: each rank skips its own shard's batches (deterministic
+            # samplers), which keeps ranks aligned — the reference skips only without DDP.
+            for _ in range(resumed_from_step * accum):
+                batches.next()
+
+        first_step_loss: float | None = None
+        final_val_loss: float | None = None
+        final_val_metrics: dict[str, float] | None = None
+        step_loss = 0.0
+        tokens_local_total = 0
+        tokens_global_total = 0
+        interval_loss = torch.zeros((), dtype=torch.float32, device=self._device)
+        interval_steps = 0
+        interval_tokens = 0
+        interval_t0 = time.perf_counter()
+        last_step_loss_dev: torch.Tensor | None = None
+        profiler = self._profiler()
+
+        for step in range(start_step, max_steps + 1):
+            if profiler is not None:
+                profiler.before_step(step)
+            self._optimizer.zero_grad()
+            step_loss_dev = torch.zeros((), dtype=torch.float32, device=self._device)
+            step_tokens = 0
+            for micro in range(accum):
+                batch = _to_device(batches.next(), self._device)
+                step_tokens += batch["input_ids"].numel()
+                with self._sync_context(micro == accum - 1):
+                    with self._policy.autocast():
+                        loss, metrics = self._adapter.compute_loss(self._model, batch)
+                    (loss / accum).backward()
+                step_loss_dev += _loss_tensor(loss, metrics)
+            self._optimizer_step()
+            if fail_at is not None and step == int(fail_at):
+                raise RuntimeError(f"fault injection: trainer.extra.fail_at_step={fail_at}")
+
+            step_loss_dev /= accum
+            last_step_loss_dev = step_loss_dev
+            tokens_local_total += step_tokens
+            if step == 1:
+                first_step_loss = float(step_loss_dev.item())
+
+            if self._ckpt_mgr is not None and self._is_main and (step % cfg.save_every_steps == 0 or step == max_steps):
+                self._ckpt_mgr.save(
+                    step, self._raw_model, self._optimizer, self._scheduler, self._cfg,
+                    extra={"world_size": self._world_size, "batches_consumed": batches.consumed},
+                )
+
+            interval_loss += step_loss_dev
+            interval_steps += 1
+            interval_tokens += step_tokens
+
+            if step % cfg.log_every_steps == 0 or step == max_steps:
+                avg_loss = float(interval_loss.item()) / interval_steps  # the interval's one sync
+                self._check_engine_flags()
+                interval_time = time.perf_counter() - interval_t0
+                step_time = interval_time / interval_steps
+                tps = interval_tokens / interval_time if interval_time > 0 else 0.0
+                lr = float(self._scheduler.get_last_lr()[0])
+                if not math.isfinite(avg_loss) and self._cfg.trainer.extra.get("halt_on_nan", True):
+                    raise FloatingPointError(f"non-finite training loss {avg_loss} at step {step}")
+                extra_metrics = self._device_metrics(tps)
+                if self._is_ddp_active:
+                    per_rank = self._gather_scalars(
+                        avg_loss=avg_loss, lr=lr, tokens_per_sec=tps, step_time=step_time,
+                        tokens_total=float(tokens_local_total),
+                    )
+                    if per_rank is not None:
+                        for r, vals in enumerate(per_rank):
+                            self._tracker.log_metrics(
+                                {
+                                    f"train/loss_rank_{r}": vals["avg_loss"],
+                                    f"train/lr_rank_{r}": vals["lr"],
+                                    f"train/tokens_per_sec_rank_{r}": vals["tokens_per_sec"],
+                                    f"train/step_time_sec_rank_{r}": vals["step_time"],
+                                    f"train/tokens_total_rank_{r}": vals["tokens_total"],
+                                },
+                                step=step,
+                            )
+                    red = self._reduce_metrics(
+                        loss_sum=float(interval_loss.item()), steps=float(interval_steps), tokens=float(interval_tokens)
+                    )
+                    if self._is_main:
+                        tokens_global_total += int(red["tokens"])
+                        global_tps = red["tokens"] / interval_time if interval_time > 0 else 0.0
+                        self._tracker.log_metrics(
+                            {
+                                "train/loss": red["loss_sum"] / red["steps"],
+                                "train/lr": lr,
+                                "train/tokens_per_sec": global_tps,
+                                "train/tokens_total": float(tokens_global_total),
+                                "train/step_time_sec": step_time,
+                                **self._device_metrics(global_tps / self._world_size),
+                            },
+                            step=step,
+                        )
+                elif self._is_main:
+                    self._tracker.log_metrics(
+                        {
+                            "train/loss": avg_loss,
+                            "train/lr": lr,
+                            "train/tokens_per_sec": tps,
+                            "train/step_time_sec": step_time,
+                            "train/tokens_total": float(tokens_local_total),
+                            **extra_metrics,
+                        },
+                        step=step,
+                    )
+                logger.info(
+                    "step=%d/%d  loss=%.4f  lr=%.6e  tokens_per_sec=%.1f  step_time=%.4fs",
+                    step, max_steps, avg_loss, lr, tps, step_time,
+                )
+                interval_loss.zero_()
+                interval_steps = 0
+                interval_tokens = 0
+                interval_t0 = time.perf_counter()
+
+            if step % cfg.eval_every_steps == 0 or step == max_steps:
+                result = self._evaluate()
+                if result is not None:
+                    local_val, global_val = result
+                    if self._is_ddp_active:
+                        per_rank = self._gather_scalars(val_loss=local_val.get("val/loss", 0.0))
+                        if per_rank is not None:
+                            for r, vals in enumerate(per_rank):
+                                self._tracker.log_metrics({f"val/loss_rank_{r}": vals["val_loss"]}, step=step)
+                    if self._is_main:
+                        self._tracker.log_metrics(global_val, step=step)
+                    effective = global_val if self._is_main else local_val
+                    if effective:
+                        final_val_metrics = effective
+                        if "val/loss" in effective:
+                            final_val_loss = effective["val/loss"]
+                        text = "  ".join(f"{k}={v:.4f}" for k, v in sorted(effective.items()))
+                        logger.info("val_step=%d/%d  %s", step, max_steps, text)
+                interval_t0 = time.perf_counter() if interval_steps == 0 else interval_t0
+            if profiler is not None:
+                profiler.after_step(step)
+
+        if last_step_loss_dev is not None:
+            step_loss = float(last_step_loss_dev.item())
+        if profiler is not None:
+            profiler.close()
+        total_time = time.perf_counter() - t_start
+        peak = 0.0
+        if self._device.type == "cuda":
+            peak = torch.cuda.max_memory_allocated(self._device) / 2**30
+        return TrainResult(
+            final_step=max_steps,
+            final_loss=step_loss,
+            final_val_loss=final_val_loss,
+            total_time=total_time,
+            peak_memory=peak,
+            val_metrics=final_val_metrics,
+            first_step_loss=first_step_loss,
+            resumed_from_step=resumed_from_step,
+            parameter_count=n_params,
+            trainable_parameter_count=n_trainable,
+        )
+
+    def _device_metrics(self, tokens_per_sec_per_gpu: float) -> dict[str, float]:
+        """GPU-only extras: model FLOPs utilisation (vs dense bf16 peak) and peak memory."""
+        if self._device.type != "cuda":
+            return {}
+        from llmtrain.utils.flops import mfu, training_flops_per_token
+
+        per_tok = training_flops_per_token(self._raw_model, self._cfg.model.block_size)
+        return {
+            "train/mfu": mfu(tokens_per_sec_per_gpu, per_tok),
+            "train/peak_mem_gb": torch.cuda.max_memory_allocated(self._device) / 2**30,
+        }

@@ -1,0 +1,129 @@
+// Fused AdamW over the flat parameter store + global gradient sum of squares (gfx950).
+//
+// Replaces reference training/trainer.py:390-394 (clip_grad_norm_ + torch.optim.AdamW.step()).
+// One grid-stride pass reads param/grad/exp_avg/exp_avg_sq as float4 and writes param,
+// both moments AND the bf16 shadow copy of the weights used by the next forward's GEMMs
+// (30 B per parameter, HBM bound).  The gradient-clipping coefficient arrives as a device
+// scalar (computed from the sumsq kernel below), so clipping costs no host round trip and
+// no extra pass over the gradients.  The update order matches torch.optim.AdamW exactly:
+//   p *= 1 - lr*wd;  m += (1-b1)(g-m);  v = b2 v + (1-b2) g^2;
+//   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+#include "common.h"
+#include "kernels.h"
+
+namespace llmt {
+namespace {
+
+struct AdamScalars {
+  float decay, one_minus_b1, b2, one_minus_b2, step_size, bc2_sqrt, eps;
+};
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamScalars& s) {
+  p *= s.decay;
+  m = fmaf(s.one_minus_b1, g - m, m);
+  v = fmaf(s.b2, v, s.one_minus_b2 * g * g);
+  const float denom = sqrtf(v) / s.bc2_sqrt + s.eps;
+  p -= s.step_size * (m / denom);
+}
+
+template <bool SHADOW_BF16>
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ param, const float* __restrict__ grad,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    void* __restrict__ shadow,
+                                                    const float* __restrict__ grad_scale, long n,
+                                                    AdamScalars s) {
+  const float gs = grad_scale != nullptr ? *grad_scale : 1.f;
+  const long n4 = n >> 2;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4_t p = reinterpret_cast<float4_t*>(param)[i];
+    float4_t g = reinterpret_cast<const float4_t*>(grad)[i] * gs;
+    float4_t mm = reinterpret_cast<float4_t*>(m)[i];
+    float4_t vv = reinterpret_cast<float4_t*>(v)[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float pk = p[k], mk = mm[k], vk = vv[k];
+      adam_elem(pk, g[k], mk, vk, s);
+      p[k] = pk; mm[k] = mk; vv[k] = vk;
+    }
+    reinterpret_cast<float4_t*>(param)[i] = p;
+    reinterpret_cast<float4_t*>(m)[i] = mm;
+    reinterpret_cast<float4_t*>(v)[i] = vv;
+    if (shadow != nullptr) {
+      if (SHADOW_BF16) {
+        ushort4_t o;
+        o[0] = f2bf(p[0]); o[1] = f2bf(p[1]); o[2] = f2bf(p[2]); o[3] = f2bf(p[3]);
+        reinterpret_cast<ushort4_t*>(shadow)[i] = o;
+      } else {
+        reinterpret_cast<float4_t*>(shadow)[i] = p;
+      }
+    }
+  }
+  // scalar tail (n % 4 elements)
+  for (long i = (n4 << 2) + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float p = param[i], mm = m[i], vv = v[i];
+    adam_elem(p, grad[i] * gs, mm, vv, s);
+    param[i] = p; m[i] = mm; v[i] = vv;
+    if (shadow != nullptr) {
+      if (SHADOW_BF16) reinterpret_cast<bf16_raw*>(shadow)[i] = f2bf(p);
+      else reinterpret_cast<float*>(shadow)[i] = p;
+    }
+  }
+}
+
+constexpr int kSumsqThreads = 256;
+
+__global__ __launch_bounds__(kSumsqThreads) void sumsq_partial_kernel(const float* __restrict__ x, long n,
+                                                                      float* __restrict__ partials) {
+  __shared__ float scratch[kSumsqThreads / 64];
+  const long n4 = n >> 2;
+  const long stride = (long)gridDim.x * blockDim.x;
+  float acc = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4_t a = reinterpret_cast<const float4_t*>(x)[i];
+    acc += a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3];
+  }
+  for (long i = (n4 << 2) + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) acc += x[i] * x[i];
+  acc = block_sum<kSumsqThreads / 64>(acc, scratch);
+  if (threadIdx.x == 0) partials[blockIdx.x] = acc;
+}
+
+// fixed-order final reduction: bitwise reproducible across runs
+__global__ __launch_bounds__(kSumsqThreads) void sumsq_final_kernel(const float* __restrict__ partials, int n,
+                                                                    float* __restrict__ out) {
+  __shared__ float scratch[kSumsqThreads / 64];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) acc += partials[i];
+  acc = block_sum<kSumsqThreads / 64>(acc, scratch);
+  if (threadIdx.x == 0) *out = acc;
+}
+
+}  // namespace
+
+hipError_t launch_adamw_flat(const AdamWArgs& a, hipStream_t stream) {
+  if (a.n <= 0) return hipSuccess;
+  AdamScalars s;
+  s.decay = 1.f - a.lr * a.weight_decay;
+  s.one_minus_b1 = 1.f - a.beta1;
+  s.b2 = a.beta2;
+  s.one_minus_b2 = 1.f - a.beta2;
+  s.step_size = a.lr / a.bias_correction1;
+  s.bc2_sqrt = a.bias_correction2_sqrt;
+  s.eps = a.eps;
+  const int grid = stride_grid((a.n + 3) / 4, 256, 256 * 8);
+  if (a.shadow_bf16)
+    hipLaunchKernelGGL(adamw_kernel<true>, dim3(grid), dim3(256), 0, stream, a.param, a.grad, a.exp_avg,
+                       a.exp_avg_sq, a.shadow, a.grad_scale, (long)a.n, s);
+  else
+    hipLaunchKernelGGL(adamw_kernel<false>, dim3(grid), dim3(256), 0, stream, a.param, a.grad, a.exp_avg,
+                       a.exp_avg_sq, a.shadow, a.grad_scale, (long)a.n, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_sumsq(const float* x, long long n, float* partials, float* out, hipStream_t stream) {
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kSumsqBlocks), dim3(kSumsqThreads), 0, stream, x, (long)n, partials);
+  hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(kSumsqThreads), 0, stream, partials, kSumsqBlocks, out);
+  return hipGetLastError();
+}
+
+}  // namespace llmt

@@ -1,0 +1,284 @@
+// Causal flash-attention backward, head_dim 64, for gfx950 (MI355X).
+//
+// Replaces the autograd backward of reference models/gpt.py:56-69 (softmax + two batched
+// matmuls over materialised [B, H, T, T] tensors).  P is recomputed from Q, K and the forward's
+// log-sum-exp; nothing of size T^2 touches memory.
+//
+// Structure (after the MI355X playbook's attention-backward recipe):
+//  * workgroup = 8 wave64s = one 256-key block of one (batch, head); wave w owns keys
+//    32w..32w+31 with the KEY ON THE MFMA LANE: its K and V fragments stay in registers and its
+//    dK^T / dV^T accumulators (2 x 32x32 f32 tiles each) live in registers for the whole sweep
+//    over query tiles, so dK and dV need no cross-workgroup reduction;
+//  * per 32-row query tile: S = Q K^T and dP = dO V^T with the accumulators PRE-LOADED with the
+//    row constants (-LSE/scale and -delta) so exp2(c*S) is P directly and dP - delta comes out
+//    of the MFMA chain; dS = P o (dP - delta);
+//  * P and dS are already the B operands of dV^T += dO^T P and dK^T += Q^T dS (accumulator used
+//    as the next MFMA's operand); dO^T and Q^T fragments come from ds_read_b64_tr_b16 on the
+//    same LDS images that serve the row reads (one swizzle, conflict free both ways);
+//  * dS crosses LDS once (as a [key][q] image written 8 bytes per lane) and dQ = dS K is formed
+//    with 16x16x32 MFMAs over the block's 256 keys, then added to an f32 dQ buffer with
+//    no-return float atomics (dQ bytes / 1.3 TB/s is the floor of this design; a 256-key block
+//    halves it vs 128).  A tiny epilogue kernel converts dQ to bf16 into the packed dqkv.
+#include "attention_common.h"
+
+namespace llmt {
+namespace attn {
+
+constexpr int kBwdWaves = 8;
+constexpr int kKvBlk = 32 * kBwdWaves;  // 256 keys per workgroup
+constexpr int kQTile = 32;
+
+// delta[b, h, t] = sum_d dO[b, t, h, d] * O[b, t, h, d]; 8 lanes per row
+__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restrict__ dout,
+                                                         const bf16_raw* __restrict__ out,
+                                                         float* __restrict__ delta, int T, int H, long rows) {
+  const long row = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 3;  // row = (b*T + t)*H + h
+  const int sub = threadIdx.x & 7;
+  float acc = 0.f;
+  if (row < rows) {
+    float a[8], o[8];
+    unpack8(*reinterpret_cast<const ushort8_t*>(dout + row * kHD + 8 * sub), a);
+    unpack8(*reinterpret_cast<const ushort8_t*>(out + row * kHD + 8 * sub), o);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc += a[i] * o[i];
+  }
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  acc += __shfl_xor(acc, 4, 64);
+  if (row < rows && sub == 0) {
+    const long bt = row / H;
+    const int h = (int)(row - bt * H);
+    const long b = bt / T, t = bt - b * T;
+    delta[(b * H + h) * T + t] = acc;
+  }
+}
+
+// dqkv[b, t, 0, h, :] = bf16(dq_accum[b, t, h, :])
+__global__ __launch_bounds__(256) void attn_dq_store_kernel(const float* __restrict__ dq, bf16_raw* __restrict__ dqkv,
+                                                            int H, long n8) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // one 8-element chunk
+  if (i >= n8) return;
+  const long row = i >> 3;  // (b*T + t)*H + h
+  const int c = (int)(i & 7);
+  const long bt = row / H;
+  const int h = (int)(row - bt * H);
+  const float4_t* src = reinterpret_cast<const float4_t*>(dq + row * kHD + 8 * c);
+  const float4_t a = src[0], b2 = src[1];
+  const float f[8] = {a[0], a[1], a[2], a[3], b2[0], b2[1], b2[2], b2[3]};
+  *reinterpret_cast<ushort8_t*>(dqkv + (bt * 3 * H + h) * kHD + 8 * c) = pack8(f);
+}
+
+__global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __restrict__ qkv,
+                                                          const bf16_raw* __restrict__ dout,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ delta,
+                                                          bf16_raw* __restrict__ dqkv,
+                                                          float* __restrict__ dq_accum, int T, int H) {
+  __shared__ __attribute__((aligned(16))) bf16_raw k_lds[kKvBlk * kHD];   // 32 KB, swizzled rows
+  __shared__ __attribute__((aligned(16))) bf16_raw q_lds[kQTile * kHD];   // 4 KB
+  __shared__ __attribute__((aligned(16))) bf16_raw do_lds[kQTile * kHD];  // 4 KB
+  __shared__ __attribute__((aligned(16))) bf16_raw ds_lds[kKvBlk * kQTile];  // 16 KB, [key][q]
+  __shared__ __attribute__((aligned(16))) float rowc_lds[2 * kQTile];      // -lse/scale | -delta
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int half = lane >> 5, col = lane & 31;
+  const int kb = blockIdx.x;
+  const int bh = blockIdx.y;
+  const int b = bh / H, h = bh - b * H;
+  const long row_stride = 3L * H * kHD;
+  const bf16_raw* base = qkv + (long)b * T * row_stride + (long)h * kHD;
+  const bf16_raw* dobase = dout + (long)b * T * H * kHD + (long)h * kHD;  // [B, T, H, 64]
+  const long out_stride = (long)H * kHD;
+  const float* lse_bh = lse + ((long)b * H + h) * T;
+  const float* delta_bh = delta + ((long)b * H + h) * T;
+
+  const int kblk0 = kb * kKvBlk;
+  const int kw0 = kblk0 + 32 * wave;  // first key of this wave
+  const int key = kw0 + col;          // this lane's key
+
+  constexpr float scale = 0.125f;
+  constexpr float c = scale * 1.4426950408889634f;
+
+  // K and V fragments of this lane's key: B operands of S = Q K^T and dP = dO V^T
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    ushort8_t kz = {0, 0, 0, 0, 0, 0, 0, 0}, vz = kz;
+    if (key < T) {
+      const bf16_raw* src = base + (long)key * row_stride + 16 * kk + 8 * half;
+      kz = *reinterpret_cast<const ushort8_t*>(src + kHD * H);
+      vz = *reinterpret_cast<const ushort8_t*>(src + 2 * kHD * H);
+    }
+    kf[kk] = __builtin_bit_cast(bf16x8, kz);
+    vf[kk] = __builtin_bit_cast(bf16x8, vz);
+  }
+  // whole 256-key K block into LDS (B operand of dQ = dS K through transposed reads)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int cidx = threadIdx.x + 512 * i;
+    const int r = cidx >> 3, ch = cidx & 7;
+    ushort8_t kz = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (kblk0 + r < T) kz = *reinterpret_cast<const ushort8_t*>(base + (long)(kblk0 + r) * row_stride + kHD * H + ch * 8);
+    *reinterpret_cast<ushort8_t*>(&k_lds[tile_chunk_off(r, ch)]) = kz;
+  }
+
+  f32x16 dk[2], dv[2];
+  dk[0] = 0.f; dk[1] = 0.f; dv[0] = 0.f; dv[1] = 0.f;
+
+  const int qt_dq = wave & 1;   // dQ output tile of this wave: q rows 16*qt_dq..
+  const int dt_dq = wave >> 1;  //                               d cols 16*dt_dq..
+
+  for (int q0 = kblk0; q0 < T; q0 += kQTile) {
+    // ---- stage Q, dO tiles and the row constants ------------------------------------
+    {
+      const int r = threadIdx.x >> 4, ch = (threadIdx.x >> 1) & 7, which = threadIdx.x & 1;
+      const int qrow = q0 + r;
+      ushort8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (qrow < T) {
+        v = which == 0 ? *reinterpret_cast<const ushort8_t*>(base + (long)qrow * row_stride + ch * 8)
+                       : *reinterpret_cast<const ushort8_t*>(dobase + (long)qrow * out_stride + ch * 8);
+      }
+      *reinterpret_cast<ushort8_t*>((which == 0 ? q_lds : do_lds) + tile_chunk_off(r, ch)) = v;
+      if (threadIdx.x < 2 * kQTile) {
+        const int t = threadIdx.x & (kQTile - 1);
+        const int qq = q0 + t;
+        float val = 0.f;
+        if (qq < T) val = threadIdx.x < kQTile ? -lse_bh[qq] / scale : -delta_bh[qq];
+        rowc_lds[threadIdx.x] = val;
+      }
+    }
+    __syncthreads();
+
+    const bool active = kw0 <= q0 + kQTile - 1 && kw0 < T;  // wave-uniform: any unmasked pair?
+    f32x16 p, ds;
+    if (active) {
+      // row constants as the initial accumulators
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const f32x4 lc = *reinterpret_cast<const f32x4*>(&rowc_lds[8 * rr + 4 * half]);
+        const f32x4 dc = *reinterpret_cast<const f32x4*>(&rowc_lds[kQTile + 8 * rr + 4 * half]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          p[4 * rr + i] = lc[i];
+          ds[4 * rr + i] = dc[i];
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const bf16x8 qa = lds_row_read(q_lds, col, 2 * kk + half);
+        p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[kk], p, 0, 0, 0);
+        const bf16x8 da = lds_row_read(do_lds, col, 2 * kk + half);
+        ds = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[kk], ds, 0, 0, 0);
+      }
+      const bool need_mask = (kw0 + 31 > q0) || (key >= T) || (q0 + kQTile > T);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float pr = exp2f(p[r] * c);
+        if (need_mask) {
+          const int qq = q0 + acc_row(r, half);
+          if (key > qq || key >= T || qq >= T) pr = 0.f;
+        }
+        p[r] = pr;
+        ds[r] = pr * ds[r];
+      }
+      // dV^T += dO^T P ; dK^T += Q^T dS  (P, dS used in place as B operands)
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8 pb = pack_acc8(p, st);
+        const bf16x8 sb = pack_acc8(ds, st);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const bf16x8 doa = lds_tr_read_operand(do_lds, 16 * st + 4 * half, dt * 32, lane);
+          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(doa, pb, dv[dt], 0, 0, 0);
+          const bf16x8 qa = lds_tr_read_operand(q_lds, 16 * st + 4 * half, dt * 32, lane);
+          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, sb, dk[dt], 0, 0, 0);
+        }
+      }
+    } else {
+      ds = 0.f;
+    }
+    // dS^T image: [key within block][q], lane writes its key's q rows 8g+4h .. +3 (8 bytes)
+    {
+      const int kl = 32 * wave + col;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        ushort4_t v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = f2bf(ds[4 * g + i]);
+        *reinterpret_cast<ushort4_t*>(&ds_lds[kl * kQTile + 8 * g + 4 * half]) = v;
+      }
+    }
+    __syncthreads();
+
+    // ---- dQ[q0 + 16 qt .., 16 dt ..] += dS K over the block's 256 keys (16x16x32 MFMA) ----
+    {
+      const int i = lane & 15, g = lane >> 4;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      constexpr int nks = kKvBlk / 32;  // keys >= T carry K = 0 and dS = 0
+#pragma unroll
+      for (int ks = 0; ks < nks; ++ks) {
+        const int key0 = 32 * ks + 8 * g + (i >> 2);
+        const int qcol = 16 * qt_dq + 4 * (i & 3);
+        const short4v a_lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)&ds_lds[key0 * kQTile + qcol]);
+        const short4v a_hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)&ds_lds[(key0 + 4) * kQTile + qcol]);
+        const int dcol = 16 * dt_dq + 4 * (i & 3);
+        const short4v b_lo = tr_read(k_lds, key0, dcol);
+        const short4v b_hi = tr_read(k_lds, key0 + 4, dcol);
+        typedef short short8v __attribute__((ext_vector_type(8)));
+        const short8v av = {a_lo[0], a_lo[1], a_lo[2], a_lo[3], a_hi[0], a_hi[1], a_hi[2], a_hi[3]};
+        const short8v bv = {b_lo[0], b_lo[1], b_lo[2], b_lo[3], b_hi[0], b_hi[1], b_hi[2], b_hi[3]};
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, bv),
+                                                      acc, 0, 0, 0);
+      }
+      const int d = 16 * dt_dq + i;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = q0 + 16 * qt_dq + 4 * g + r;
+        if (qq < T) atomicAdd(&dq_accum[(((long)b * T + qq) * H + h) * kHD + d], acc[r] * scale);
+      }
+    }
+    // no barrier needed here: the next tile's staging writes only q/do/rowc (not read in the
+    // dQ phase) and its dS writes come after the next barrier
+  }
+
+  // ---- dK = scale * dK^T, dV = dV^T  -> dqkv[b, key, 1|2, h, :] ------------------------------
+  if (key < T) {
+    bf16_raw* dst = dqkv + ((long)b * T + key) * row_stride + (long)h * kHD;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        ushort4_t kv, vv;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          kv[i] = f2bf(dk[dt][4 * g + i] * scale);
+          vv[i] = f2bf(dv[dt][4 * g + i]);
+        }
+        const int d = dt * 32 + 8 * g + 4 * half;
+        *reinterpret_cast<ushort4_t*>(dst + kHD * H + d) = kv;
+        *reinterpret_cast<ushort4_t*>(dst + 2 * kHD * H + d) = vv;
+      }
+    }
+  }
+}
+
+}  // namespace attn
+
+hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse, void* dqkv,
+                           float* delta, float* dq_accum, int B, int T, int H, hipStream_t stream) {
+  if (B <= 0 || T <= 0 || H <= 0) return hipErrorInvalidValue;
+  const long rows = (long)B * T * H;
+  hipError_t e = hipMemsetAsync(dq_accum, 0, rows * attn::kHD * sizeof(float), stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, stream,
+                     (const bf16_raw*)dout, (const bf16_raw*)out, delta, T, H, rows);
+  const int nkb = (T + attn::kKvBlk - 1) / attn::kKvBlk;
+  hipLaunchKernelGGL(attn::attn_bwd_kernel, dim3(nkb, B * H), dim3(512), 0, stream, (const bf16_raw*)qkv,
+                     (const bf16_raw*)dout, lse, delta, (bf16_raw*)dqkv, dq_accum, T, H);
+  const long n8 = rows * attn::kHD / 8;
+  hipLaunchKernelGGL(attn::attn_dq_store_kernel, dim3((n8 + 255) / 256), dim3(256), 0, stream, dq_accum,
+                     (bf16_raw*)dqkv, H, n8);
+  return hipGetLastError();
+}
+
+}  // namespace llmt

@@ -1,0 +1,70 @@
+// Shared pieces of the gfx950 flash-attention kernels (head_dim 64).
+#pragma once
+
+#include "common.h"
+#include "kernels.h"
+
+namespace llmt {
+namespace attn {
+
+constexpr int kHD = 64;  // head dim: one 128-byte bf16 row per key/query
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) short4v lds_short4;
+
+// LDS image of a [rows][64] bf16 tile: 128-byte rows of eight 16-byte chunks, chunk index
+// XOR-swizzled by g((row >> 1) & 7) with g(k) = ((k & 1) << 2) | (k >> 1).
+//  * row reads (ds_read_b128; 16 lanes = 16 distinct rows mod 16, one chunk): slot
+//    (row & 1) * 8 + (ch ^ g) is a bijection over those rows -> conflict free;
+//  * transposed reads (ds_read_b64_tr_b16; rows r0..r0+3, r0 % 4 == 0, four aligned chunks):
+//    g(2m) ^ g(2m + 1) == 4 moves rows r0+2/r0+3 to the other half of the 256-byte bank row
+//    -> conflict free.
+__device__ __forceinline__ int swz(int row, int ch) {
+  const int k = (row >> 1) & 7;
+  return ch ^ (((k & 1) << 2) | (k >> 1));
+}
+__device__ __forceinline__ int tile_chunk_off(int row, int ch) { return row * kHD + (swz(row, ch) << 3); }
+__device__ __forceinline__ int tile_elem_off(int row, int col) {
+  return row * kHD + (swz(row, col >> 3) << 3) + (col & 7);
+}
+
+// 8 contiguous bf16 of one row (an MFMA A/B fragment with k along the row)
+__device__ __forceinline__ bf16x8 lds_row_read(const bf16_raw* tile, int row, int ch) {
+  return *reinterpret_cast<const bf16x8*>(tile + tile_chunk_off(row, ch));
+}
+
+__device__ __forceinline__ short4v tr_read(const bf16_raw* tile, int row, int col) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(tile + tile_elem_off(row, col)));
+}
+
+// 32x32x16 MFMA operand whose k index runs DOWN the tile's rows (e.g. V^T with k = key):
+// lane l gets column (dcol_base + (l & 31)) and rows row_base + {0..3} (elements 0..3) and
+// row_base + 8 + {0..3} (elements 4..7) — the k order of an accumulator used as the other
+// operand ("element j of lane half h is row 16s + 8(j>>2) + 4h + (j&3)"); callers fold the
+// 16s + 4h part into row_base.
+__device__ __forceinline__ bf16x8 lds_tr_read_operand(const bf16_raw* tile, int row_base, int dcol_base, int lane) {
+  const int i = lane & 15;
+  const int col = dcol_base + 16 * ((lane >> 4) & 1) + 4 * (i & 3);
+  const short4v lo = tr_read(tile, row_base + (i >> 2), col);
+  const short4v hi = tr_read(tile, row_base + 8 + (i >> 2), col);
+  typedef short short8v __attribute__((ext_vector_type(8)));
+  const short8v all = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, all);
+}
+
+// row (within a 32x32 accumulator tile) held in register r by lane half `half`
+__device__ __forceinline__ int acc_row(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
+
+// registers 8*st .. 8*st+7 of an accumulator -> bf16 fragment for k-step st
+__device__ __forceinline__ bf16x8 pack_acc8(const f32x16& acc, int st) {
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = static_cast<__bf16>(acc[8 * st + j]);
+  return v;
+}
+
+}  // namespace attn
+}  // namespace llmt

@@ -1,0 +1,199 @@
+// Causal flash-attention forward, head_dim 64, bf16 in / bf16 out, for gfx950 (MI355X).
+//
+// Replaces reference models/gpt.py:49-71 (qkv split, Q K^T / sqrt(hd), causal masked_fill,
+// softmax, P V), which materialises [B, H, T, T] fp32 scores; here nothing of size T^2 ever
+// reaches memory and the kernel reads Q/K/V straight out of the packed projection output
+// qkv[B, T, 3, H, 64] (no transpose/contiguous copies) and writes out[B, T, H, 64], i.e. the
+// exact operand layout of the following out_proj GEMM.
+//
+// Structure (CDNA4 idioms from the MI355X playbook):
+//  * workgroup = 4 wave64s = a 128-row query block; each wave owns 32 query rows and keeps its
+//    Q fragments in registers for the whole key sweep;
+//  * "swapped" S^T = K Q^T with v_mfma_f32_32x32x16_bf16: the query index lands on the MFMA
+//    lane, so the online-softmax row max / row sum are lane-local (one xor-32 shuffle joins the
+//    two lane halves) and the running O^T accumulator is rescaled without any cross-lane move;
+//  * the S^T accumulator is converted to bf16 in registers and used directly as the B operand
+//    of O^T += V^T P^T (no LDS round trip for P); V^T fragments come from LDS through the gfx950
+//    transposing read ds_read_b64_tr_b16;
+//  * K/V tiles of 64 keys are double-buffered in LDS with register staging (loads for tile
+//    i+1 are issued before the MFMAs of tile i and written after them: one barrier per tile);
+//  * one XOR swizzle of the 16-byte chunks of each 128-byte LDS row makes both the row reads
+//    (ds_read_b128, K as the A operand) and the transposed reads (V) bank-conflict free;
+//  * softmax in the exp2 domain (v_exp_f32), scale folded into one multiply;
+//  * heaviest (last) query blocks are dispatched first to shorten the causal tail.
+#include "attention_common.h"
+
+namespace llmt {
+namespace attn {
+
+constexpr int kFwdWaves = 4;
+constexpr int kQBlk = 32 * kFwdWaves;  // 128 query rows per workgroup
+constexpr int kKBlk = 64;              // keys per LDS tile
+
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __restrict__ qkv,
+                                                          bf16_raw* __restrict__ out,
+                                                          float* __restrict__ lse, int T, int H,
+                                                          int nqb) {
+  __shared__ __attribute__((aligned(16))) bf16_raw smem[2][2][kKBlk * kHD];  // [buf][K|V][tile]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int half = lane >> 5, col = lane & 31;
+  const int qb = nqb - 1 - (int)blockIdx.x;  // heavy blocks first
+  const int bh = blockIdx.y;
+  const int b = bh / H, h = bh - b * H;
+  const long row_stride = 3L * H * kHD;  // elements between consecutive tokens in qkv
+  const bf16_raw* base = qkv + (long)b * T * row_stride + (long)h * kHD;
+
+  const int q0w = qb * kQBlk + wave * 32;   // first query row of this wave
+  const int q = q0w + col;                   // this lane's query row
+  const int q_hi = min(q0w + 31, T - 1);     // last valid query row of the wave
+
+  // Q fragments (B operand of S^T = K Q^T): lane holds Q[q][16kk + 8*half + 0..7]
+  bf16x8 qf[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    ushort8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (q < T) v = *reinterpret_cast<const ushort8_t*>(base + (long)q * row_stride + 16 * kk + 8 * half);
+    qf[kk] = __builtin_bit_cast(bf16x8, v);
+  }
+
+  const int kv_end = min(T, qb * kQBlk + kQBlk);
+  const int ntiles = (kv_end + kKBlk - 1) / kKBlk;
+
+  // register staging of one K/V tile: 512 16-byte chunks each, 2 per thread
+  ushort8_t stage[4];
+  auto load_tile = [&](int tile) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int r = c >> 3, ch = c & 7;
+      const int key = tile * kKBlk + r;
+      ushort8_t kz = {0, 0, 0, 0, 0, 0, 0, 0}, vz = kz;
+      if (key < T) {
+        const bf16_raw* src = base + (long)key * row_stride + ch * 8;
+        kz = *reinterpret_cast<const ushort8_t*>(src + kHD * H);
+        vz = *reinterpret_cast<const ushort8_t*>(src + 2 * kHD * H);
+      }
+      stage[i] = kz;
+      stage[2 + i] = vz;
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int r = c >> 3, ch = c & 7;
+      const int off = tile_chunk_off(r, ch);
+      *reinterpret_cast<ushort8_t*>(&smem[buf][0][off]) = stage[i];
+      *reinterpret_cast<ushort8_t*>(&smem[buf][1][off]) = stage[2 + i];
+    }
+  };
+
+  f32x16 o[2];
+  o[0] = 0.f;
+  o[1] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+  constexpr float c = 0.125f * 1.4426950408889634f;  // (1/sqrt(64)) * log2(e)
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int cur = it & 1;
+    const bool more = it + 1 < ntiles;
+    if (more) load_tile(it + 1);
+    const int kbase = it * kKBlk;
+    if (kbase <= q_hi) {
+      const bf16_raw* Kt = smem[cur][0];
+      const bf16_raw* Vt = smem[cur][1];
+      f32x16 s[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        s[kt] = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const bf16x8 a = lds_row_read(Kt, kt * 32 + col, 2 * kk + half);
+          s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[kk], s[kt], 0, 0, 0);
+        }
+      }
+      // scale (+ causal / sequence-end mask on diagonal tiles), tile max
+      const bool need_mask = (kbase + kKBlk - 1 > q0w) || (kbase + kKBlk > T);
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float t = s[kt][r] * c;
+          if (need_mask) {
+            const int key = kbase + kt * 32 + acc_row(r, half);
+            if (key > q || key >= T) t = -INFINITY;
+          }
+          s[kt][r] = t;
+          tmax = fmaxf(tmax, t);
+        }
+      }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float m_new = fmaxf(m_run, tmax);
+      const float alpha = exp2f(m_run - m_new);
+      float psum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = exp2f(s[kt][r] - m_new);
+          s[kt][r] = p;
+          psum += p;
+        }
+      }
+      psum += __shfl_xor(psum, 32, 64);
+      l_run = l_run * alpha + psum;
+      m_run = m_new;
+      o[0] *= alpha;
+      o[1] *= alpha;
+      // O^T += V^T P^T: P^T (the S^T accumulator) is the B operand straight from registers
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const bf16x8 pb = pack_acc8(s[kt], st);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            const bf16x8 va = lds_tr_read_operand(Vt, kt * 32 + 16 * st + 4 * half, dt * 32, lane);
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o[dt], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (more) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  if (q < T) {
+    const float inv_l = 1.f / l_run;
+    bf16_raw* dst = out + ((long)b * T + q) * H * kHD + (long)h * kHD;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        ushort4_t v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = f2bf(o[dt][4 * g + i] * inv_l);
+        *reinterpret_cast<ushort4_t*>(dst + dt * 32 + 8 * g + 4 * half) = v;
+      }
+    }
+    if (half == 0) lse[((long)b * H + h) * T + q] = (m_run + log2f(l_run)) * 0.6931471805599453f;
+  }
+}
+
+}  // namespace attn
+
+hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H, hipStream_t stream) {
+  if (B <= 0 || T <= 0 || H <= 0) return hipErrorInvalidValue;
+  const int nqb = (T + attn::kQBlk - 1) / attn::kQBlk;
+  dim3 grid(nqb, B * H);
+  hipLaunchKernelGGL(attn::attn_fwd_kernel, grid, dim3(256), 0, stream, (const bf16_raw*)qkv, (bf16_raw*)out, lse,
+                     T, H, nqb);
+  return hipGetLastError();
+}
+
+}  // namespace llmt

@@ -1,0 +1,375 @@
+// torch.library registration of the llmtrain gfx950 kernels: torch.ops.llmtrain_hip.*
+//
+// Each op validates device / dtype / contiguity / shape on the host, allocates its outputs with
+// the caching allocator and launches on the current HIP stream (so ops compose with RCCL's
+// stream-ordered collectives and can be captured in a hipGraph).  Kernels are registered for
+// the CUDA dispatch key, which is how PyTorch-ROCm names HIP devices.
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+
+#include <torch/library.h>
+
+#include <cmath>
+
+#include "kernels.h"
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+void check_hip(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "llmtrain_hip: ", what, " failed: ", hipGetErrorString(e));
+}
+
+void check_gpu(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "llmtrain_hip: ", name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), "llmtrain_hip: ", name, " must be contiguous");
+}
+
+void check_dtype(const Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.scalar_type() == dt, "llmtrain_hip: ", name, " must be ", dt, ", got ", t.scalar_type());
+}
+
+bool is_lowp(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat, "llmtrain_hip: ", name,
+              " must be bf16 or f32");
+  return t.scalar_type() == at::kBFloat16;
+}
+
+// ---- LayerNorm -----------------------------------------------------------------------------
+std::tuple<Tensor, Tensor, Tensor, Tensor> add_layernorm_fwd(const Tensor& x, const c10::optional<Tensor>& delta,
+                                                             const Tensor& w, const Tensor& b, double eps,
+                                                             at::ScalarType out_dtype) {
+  check_gpu(x, "x");
+  check_dtype(x, at::kFloat, "x");
+  check_gpu(w, "weight");
+  check_gpu(b, "bias");
+  check_dtype(w, at::kFloat, "weight");
+  check_dtype(b, at::kFloat, "bias");
+  TORCH_CHECK(x.dim() == 2, "x must be [M, d]");
+  const int64_t M = x.size(0), d = x.size(1);
+  TORCH_CHECK(w.numel() == d && b.numel() == d, "weight/bias must have d elements");
+  TORCH_CHECK(d % 4 == 0 && d <= 2048, "LayerNorm kernel needs d % 4 == 0 and d <= 2048");
+  TORCH_CHECK(out_dtype == at::kBFloat16 || out_dtype == at::kFloat, "out_dtype must be bf16 or f32");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  llmt::LnFwdArgs a{};
+  Tensor xs;
+  if (delta.has_value()) {
+    check_gpu(*delta, "delta");
+    TORCH_CHECK(delta->sizes() == x.sizes(), "delta must match x");
+    a.delta = delta->data_ptr();
+    a.delta_bf16 = is_lowp(*delta, "delta");
+    xs = at::empty_like(x);
+    a.xs_out = xs.data_ptr<float>();
+  } else {
+    xs = at::empty({0}, x.options());
+  }
+  Tensor y = at::empty({M, d}, x.options().dtype(out_dtype));
+  Tensor mean = at::empty({M}, x.options());
+  Tensor rstd = at::empty({M}, x.options());
+  a.x = x.data_ptr<float>();
+  a.w = w.data_ptr<float>();
+  a.b = b.data_ptr<float>();
+  a.y = y.data_ptr();
+  a.y_bf16 = out_dtype == at::kBFloat16;
+  a.mean = mean.data_ptr<float>();
+  a.rstd = rstd.data_ptr<float>();
+  a.M = (int)M;
+  a.d = (int)d;
+  a.eps = (float)eps;
+  if (M > 0) check_hip(llmt::launch_add_layernorm_fwd(a, cur_stream()), "add_layernorm_fwd");
+  return {xs, y, mean, rstd};
+}
+
+std::tuple<Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor& xs, const Tensor& mean, const Tensor& rstd,
+                                         const Tensor& w, const c10::optional<Tensor>& dresid, Tensor dw, Tensor db,
+                                         const c10::optional<Tensor>& dy_scale, bool want_lowp,
+                                         const c10::optional<Tensor>& dproj) {
+  check_gpu(dy, "dy");
+  check_gpu(xs, "xs");
+  check_dtype(xs, at::kFloat, "xs");
+  TORCH_CHECK(dy.sizes() == xs.sizes() && xs.dim() == 2, "dy/xs must be [M, d]");
+  const int64_t M = xs.size(0), d = xs.size(1);
+  TORCH_CHECK(d % 4 == 0 && d <= 2048, "LayerNorm kernel needs d % 4 == 0 and d <= 2048");
+  for (const Tensor* t : {&mean, &rstd}) {
+    check_gpu(*t, "mean/rstd");
+    check_dtype(*t, at::kFloat, "mean/rstd");
+    TORCH_CHECK(t->numel() == M, "mean/rstd must have M elements");
+  }
+  for (const Tensor* t : {&w, static_cast<const Tensor*>(&dw), static_cast<const Tensor*>(&db)}) {
+    check_gpu(*t, "weight/dweight/dbias");
+    check_dtype(*t, at::kFloat, "weight/dweight/dbias");
+    TORCH_CHECK(t->numel() == d, "weight/dweight/dbias must have d elements");
+  }
+  at::hip::HIPGuardMasqueradingAsCUDA guard(xs.device());
+  llmt::LnBwdArgs a{};
+  a.dy = dy.data_ptr();
+  a.dy_bf16 = is_lowp(dy, "dy");
+  a.xs = xs.data_ptr<float>();
+  a.mean = mean.data_ptr<float>();
+  a.rstd = rstd.data_ptr<float>();
+  a.w = w.data_ptr<float>();
+  if (dresid.has_value()) {
+    check_gpu(*dresid, "dresid");
+    check_dtype(*dresid, at::kFloat, "dresid");
+    TORCH_CHECK(dresid->sizes() == xs.sizes(), "dresid must match xs");
+    a.dresid = dresid->data_ptr<float>();
+  }
+  if (dy_scale.has_value()) {
+    check_gpu(*dy_scale, "dy_scale");
+    check_dtype(*dy_scale, at::kFloat, "dy_scale");
+    TORCH_CHECK(dy_scale->numel() == 1, "dy_scale must be a scalar");
+    a.dy_scale = dy_scale->data_ptr<float>();
+  }
+  Tensor dx = at::empty_like(xs);
+  Tensor dx_lp = want_lowp ? at::empty_like(dy) : at::empty({0}, dy.options());
+  a.dx = dx.data_ptr<float>();
+  a.dx_lp = want_lowp ? dx_lp.data_ptr() : nullptr;
+  a.dw = dw.data_ptr<float>();
+  a.db = db.data_ptr<float>();
+  if (dproj.has_value()) {
+    check_gpu(*dproj, "dproj_bias");
+    check_dtype(*dproj, at::kFloat, "dproj_bias");
+    TORCH_CHECK(dproj->numel() == d, "dproj_bias must have d elements");
+    a.dproj = dproj->data_ptr<float>();
+  }
+  a.M = (int)M;
+  a.d = (int)d;
+  if (M > 0) check_hip(llmt::launch_layernorm_bwd(a, cur_stream()), "layernorm_bwd");
+  return {dx, dx_lp};
+}
+
+// ---- cross-entropy ---------------------------------------------------------------------------
+Tensor cross_entropy_fwd_bwd(Tensor logits, const Tensor& labels, int64_t vocab, const Tensor& row_weight) {
+  check_gpu(logits, "logits");
+  check_gpu(labels, "labels");
+  check_gpu(row_weight, "row_weight");
+  check_dtype(labels, at::kLong, "labels");
+  check_dtype(row_weight, at::kFloat, "row_weight");
+  TORCH_CHECK(logits.dim() == 2, "logits must be [M, Vp]");
+  const int64_t M = logits.size(0), Vp = logits.size(1);
+  TORCH_CHECK(labels.numel() == M && row_weight.numel() == M, "labels/row_weight must have M elements");
+  TORCH_CHECK(vocab > 0 && vocab <= Vp && Vp % 8 == 0 && Vp <= 131072, "need 0 < vocab <= Vp, Vp % 8 == 0");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
+  Tensor loss = at::empty({M}, row_weight.options());
+  if (M > 0)
+    check_hip(llmt::launch_cross_entropy_fwd_bwd(logits.data_ptr(), is_lowp(logits, "logits"),
+                                                 labels.data_ptr<int64_t>(), row_weight.data_ptr<float>(),
+                                                 loss.data_ptr<float>(), (int)M, (int)Vp, (int)vocab, cur_stream()),
+              "cross_entropy_fwd_bwd");
+  return loss;
+}
+
+// ---- elementwise -----------------------------------------------------------------------------
+Tensor gelu_fwd(const Tensor& u) {
+  check_gpu(u, "u");
+  TORCH_CHECK(u.numel() % 8 == 0, "gelu needs numel % 8 == 0");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(u.device());
+  Tensor g = at::empty_like(u);
+  if (u.numel() > 0)
+    check_hip(llmt::launch_gelu_fwd(u.data_ptr(), g.data_ptr(), is_lowp(u, "u"), u.numel(), cur_stream()), "gelu_fwd");
+  return g;
+}
+
+Tensor gelu_bwd(const Tensor& dg, const Tensor& u, const c10::optional<Tensor>& dbias) {
+  check_gpu(dg, "dg");
+  check_gpu(u, "u");
+  TORCH_CHECK(dg.sizes() == u.sizes() && u.dim() == 2, "dg/u must be [M, F]");
+  TORCH_CHECK(dg.scalar_type() == u.scalar_type(), "dg/u dtype mismatch");
+  const int64_t M = u.size(0), F = u.size(1);
+  TORCH_CHECK(F % 8 == 0, "gelu_bwd needs F % 8 == 0");
+  float* db = nullptr;
+  if (dbias.has_value()) {
+    check_gpu(*dbias, "dbias");
+    check_dtype(*dbias, at::kFloat, "dbias");
+    TORCH_CHECK(dbias->numel() == F, "dbias must have F elements");
+    db = dbias->data_ptr<float>();
+  }
+  at::hip::HIPGuardMasqueradingAsCUDA guard(u.device());
+  Tensor du = at::empty_like(u);
+  if (M > 0)
+    check_hip(llmt::launch_gelu_bwd(dg.data_ptr(), u.data_ptr(), du.data_ptr(), db, is_lowp(u, "u"), (int)M, (int)F,
+                                    cur_stream()),
+              "gelu_bwd");
+  return du;
+}
+
+void colsum_accum(const Tensor& dy, Tensor out) {
+  check_gpu(dy, "dy");
+  check_gpu(out, "out");
+  check_dtype(out, at::kFloat, "out");
+  TORCH_CHECK(dy.dim() == 2 && out.numel() == dy.size(1), "dy [M, N], out [N]");
+  TORCH_CHECK(dy.size(1) % 8 == 0, "colsum needs N % 8 == 0");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  if (dy.size(0) > 0)
+    check_hip(llmt::launch_colsum_accum(dy.data_ptr(), is_lowp(dy, "dy"), out.data_ptr<float>(), (int)dy.size(0),
+                                        (int)dy.size(1), cur_stream()),
+              "colsum_accum");
+}
+
+Tensor embedding_fwd(const Tensor& ids, const Tensor& wte, const Tensor& wpe) {
+  check_gpu(ids, "ids");
+  check_gpu(wte, "wte");
+  check_gpu(wpe, "wpe");
+  check_dtype(ids, at::kLong, "ids");
+  check_dtype(wte, at::kFloat, "wte");
+  check_dtype(wpe, at::kFloat, "wpe");
+  TORCH_CHECK(ids.dim() == 2, "ids must be [B, T]");
+  const int64_t B = ids.size(0), T = ids.size(1), d = wte.size(1);
+  TORCH_CHECK(wpe.size(1) == d && wpe.size(0) >= T && d % 4 == 0, "embedding shapes");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(ids.device());
+  Tensor x = at::empty({B * T, d}, wte.options());
+  if (B * T > 0)
+    check_hip(llmt::launch_embedding_fwd(ids.data_ptr<int64_t>(), wte.data_ptr<float>(), wpe.data_ptr<float>(),
+                                         x.data_ptr<float>(), (int)B, (int)T, (int)d, (int)wte.size(0), cur_stream()),
+              "embedding_fwd");
+  return x;
+}
+
+void embedding_bwd(const Tensor& dx, const Tensor& ids, Tensor dwte, Tensor dwpe) {
+  check_gpu(dx, "dx");
+  check_gpu(ids, "ids");
+  check_gpu(dwte, "dwte");
+  check_gpu(dwpe, "dwpe");
+  check_dtype(dx, at::kFloat, "dx");
+  check_dtype(ids, at::kLong, "ids");
+  check_dtype(dwte, at::kFloat, "dwte");
+  check_dtype(dwpe, at::kFloat, "dwpe");
+  const int64_t B = ids.size(0), T = ids.size(1), d = dwte.size(1);
+  TORCH_CHECK(dx.size(0) == B * T && dx.size(1) == d && dwpe.size(0) >= T && dwpe.size(1) == d, "embedding shapes");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dx.device());
+  if (B * T > 0)
+    check_hip(llmt::launch_embedding_bwd(dx.data_ptr<float>(), ids.data_ptr<int64_t>(), dwte.data_ptr<float>(),
+                                         dwpe.data_ptr<float>(), (int)B, (int)T, (int)d, (int)dwte.size(0),
+                                         cur_stream()),
+              "embedding_bwd");
+}
+
+// ---- attention -------------------------------------------------------------------------------
+void check_qkv(const Tensor& qkv, int64_t B, int64_t T, int64_t H) {
+  check_gpu(qkv, "qkv");
+  check_dtype(qkv, at::kBFloat16, "qkv");
+  TORCH_CHECK(qkv.numel() == B * T * 3 * H * 64, "qkv must be [B*T, 3*H*64] (head_dim 64 only)");
+}
+
+std::tuple<Tensor, Tensor> attn_fwd(const Tensor& qkv, int64_t B, int64_t T, int64_t H) {
+  check_qkv(qkv, B, T, H);
+  at::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
+  Tensor out = at::empty({B * T, H * 64}, qkv.options());
+  Tensor lse = at::empty({B, H, T}, qkv.options().dtype(at::kFloat));
+  check_hip(llmt::launch_attn_fwd(qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(), (int)B, (int)T, (int)H,
+                                  cur_stream()),
+            "attn_fwd");
+  return {out, lse};
+}
+
+Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const Tensor& lse, int64_t B, int64_t T,
+                int64_t H) {
+  check_qkv(qkv, B, T, H);
+  for (const Tensor* t : {&dout, &out}) {
+    check_gpu(*t, "dout/out");
+    check_dtype(*t, at::kBFloat16, "dout/out");
+    TORCH_CHECK(t->numel() == B * T * H * 64, "dout/out must be [B*T, H*64]");
+  }
+  check_gpu(lse, "lse");
+  check_dtype(lse, at::kFloat, "lse");
+  TORCH_CHECK(lse.numel() == B * H * T, "lse must be [B, H, T]");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
+  Tensor dqkv = at::empty_like(qkv);
+  Tensor delta = at::empty({B, H, T}, lse.options());
+  Tensor dq = at::empty({B * T * H * 64}, lse.options());
+  check_hip(llmt::launch_attn_bwd(dout.data_ptr(), qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
+                                  dqkv.data_ptr(), delta.data_ptr<float>(), dq.data_ptr<float>(), (int)B, (int)T,
+                                  (int)H, cur_stream()),
+            "attn_bwd");
+  return dqkv;
+}
+
+// ---- optimizer -------------------------------------------------------------------------------
+Tensor sumsq(const Tensor& x) {
+  check_gpu(x, "x");
+  check_dtype(x, at::kFloat, "x");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor partials = at::empty({llmt::kSumsqBlocks}, x.options());
+  Tensor out = at::empty({}, x.options());
+  check_hip(llmt::launch_sumsq(x.data_ptr<float>(), x.numel(), partials.data_ptr<float>(), out.data_ptr<float>(),
+                               cur_stream()),
+            "sumsq");
+  return out;
+}
+
+void adamw_flat(Tensor param, const Tensor& grad, Tensor exp_avg, Tensor exp_avg_sq, const c10::optional<Tensor>& shadow,
+                double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
+                const c10::optional<Tensor>& grad_scale) {
+  for (const Tensor* t : {static_cast<const Tensor*>(&param), &grad, static_cast<const Tensor*>(&exp_avg), static_cast<const Tensor*>(&exp_avg_sq)}) {
+    check_gpu(*t, "adamw buffer");
+    check_dtype(*t, at::kFloat, "adamw buffer");
+    TORCH_CHECK(t->numel() == param.numel(), "adamw buffers must have equal numel");
+  }
+  TORCH_CHECK(step >= 1, "adamw step must be >= 1");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(param.device());
+  llmt::AdamWArgs a{};
+  a.param = param.data_ptr<float>();
+  a.grad = grad.data_ptr<float>();
+  a.exp_avg = exp_avg.data_ptr<float>();
+  a.exp_avg_sq = exp_avg_sq.data_ptr<float>();
+  if (shadow.has_value()) {
+    check_gpu(*shadow, "shadow");
+    TORCH_CHECK(shadow->numel() >= param.numel(), "shadow too small");
+    a.shadow = shadow->data_ptr();
+    a.shadow_bf16 = is_lowp(*shadow, "shadow");
+  }
+  if (grad_scale.has_value()) {
+    check_gpu(*grad_scale, "grad_scale");
+    check_dtype(*grad_scale, at::kFloat, "grad_scale");
+    a.grad_scale = grad_scale->data_ptr<float>();
+  }
+  a.n = param.numel();
+  a.lr = (float)lr;
+  a.beta1 = (float)beta1;
+  a.beta2 = (float)beta2;
+  a.eps = (float)eps;
+  a.weight_decay = (float)weight_decay;
+  a.bias_correction1 = (float)(1.0 - std::pow(beta1, (double)step));
+  a.bias_correction2_sqrt = (float)std::sqrt(1.0 - std::pow(beta2, (double)step));
+  check_hip(llmt::launch_adamw_flat(a, cur_stream()), "adamw_flat");
+}
+
+}  // namespace
+
+TORCH_LIBRARY(llmtrain_hip, m) {
+  m.def("add_layernorm_fwd(Tensor x, Tensor? delta, Tensor weight, Tensor bias, float eps, ScalarType out_dtype)"
+        " -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("layernorm_bwd(Tensor dy, Tensor xs, Tensor mean, Tensor rstd, Tensor weight, Tensor? dresid,"
+        " Tensor(a!) dweight, Tensor(b!) dbias, Tensor? dy_scale, bool want_lowp, Tensor(c!)? dproj_bias)"
+        " -> (Tensor, Tensor)");
+  m.def("cross_entropy_fwd_bwd(Tensor(a!) logits, Tensor labels, int vocab, Tensor row_weight) -> Tensor");
+  m.def("gelu_fwd(Tensor u) -> Tensor");
+  m.def("gelu_bwd(Tensor dg, Tensor u, Tensor(a!)? dbias) -> Tensor");
+  m.def("colsum_accum(Tensor dy, Tensor(a!) out) -> ()");
+  m.def("embedding_fwd(Tensor ids, Tensor wte, Tensor wpe) -> Tensor");
+  m.def("embedding_bwd(Tensor dx, Tensor ids, Tensor(a!) dwte, Tensor(b!) dwpe) -> ()");
+  m.def("attn_fwd(Tensor qkv, int B, int T, int H) -> (Tensor, Tensor)");
+  m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, int B, int T, int H) -> Tensor");
+  m.def("sumsq(Tensor x) -> Tensor");
+  m.def("adamw_flat(Tensor(a!) param, Tensor grad, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor(d!)? shadow,"
+        " float lr, float beta1, float beta2, float eps, float weight_decay, int step, Tensor? grad_scale) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(llmtrain_hip, CUDA, m) {
+  m.impl("add_layernorm_fwd", &add_layernorm_fwd);
+  m.impl("layernorm_bwd", &layernorm_bwd);
+  m.impl("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd);
+  m.impl("gelu_fwd", &gelu_fwd);
+  m.impl("gelu_bwd", &gelu_bwd);
+  m.impl("colsum_accum", &colsum_accum);
+  m.impl("embedding_fwd", &embedding_fwd);
+  m.impl("embedding_bwd", &embedding_bwd);
+  m.impl("attn_fwd", &attn_fwd);
+  m.impl("attn_bwd", &attn_bwd);
+  m.impl("sumsq", &sumsq);
+  m.impl("adamw_flat", &adamw_flat);
+}

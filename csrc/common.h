@@ -1,0 +1,93 @@
+// Shared device helpers for the llmtrain gfx950 (MI355X, CDNA4) kernels.
+//
+// Conventions: wave64 everywhere (CDNA wavefront = 64 lanes), bf16 held as raw 16-bit values
+// in vector registers and converted with clang's native __bf16 type (hipcc emits
+// v_cvt_pk_bf16_f32 for the f32->bf16 direction, round-to-nearest-even, NaN preserving), global
+// memory moved in 16-byte vectors (Guideline 13: bf16 must never be loaded scalar).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace llmt {
+
+constexpr int kWave = 64;
+
+typedef unsigned short bf16_raw;
+typedef float float4_t __attribute__((ext_vector_type(4)));
+typedef float float2_t __attribute__((ext_vector_type(2)));
+typedef unsigned short ushort8_t __attribute__((ext_vector_type(8)));
+typedef unsigned short ushort4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(bf16_raw v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+__device__ __forceinline__ bf16_raw f2bf(float f) {
+  __bf16 b = static_cast<__bf16>(f);
+  return __builtin_bit_cast(bf16_raw, b);
+}
+
+// 8 x bf16 <-> 8 x f32
+__device__ __forceinline__ void unpack8(const ushort8_t v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = bf2f(v[i]);
+}
+__device__ __forceinline__ ushort8_t pack8(const float* f) {
+  ushort8_t v;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = f2bf(f[i]);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
+// Block-wide sum for blockDim.x = 64 * NWAVES; `scratch` must hold NWAVES floats.
+template <int NWAVES>
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int w = 0; w < NWAVES; ++w) r += scratch[w];
+  return r;
+}
+
+template <int NWAVES>
+__device__ __forceinline__ float block_max(float v, float* scratch) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float r = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < NWAVES; ++w) r = fmaxf(r, scratch[w]);
+  return r;
+}
+
+// Number of workgroups for a grid-stride memory-bound kernel: enough to fill 256 CUs several
+// times over without launching millions of tiny blocks (Guideline 11).
+inline int stride_grid(long long work_items, int per_block, int cap = 256 * 8) {
+  long long g = (work_items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+}  // namespace llmt

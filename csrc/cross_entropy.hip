@@ -1,0 +1,150 @@
+// Fused softmax-cross-entropy forward + gradient, one pass over the logits (gfx950).
+//
+// Replaces reference models/gpt.py:256-269 (F.cross_entropy(reduction="none") + masked mean)
+// and the autograd backward of that op.  The LM-head logits [M, Vp] (Vp = vocab padded to a
+// multiple of 64) are read ONCE into registers — 512 threads per row, each lane holding
+// ceil(Vp / 4096) 16-byte vectors — the row's log-sum-exp is reduced in the log2 domain
+// (v_exp_f32 is exp2), and the row is overwritten in place with
+//     dlogits = (softmax(z) - onehot(label)) * row_weight[row]      (0 for padded columns)
+// so the backward never touches the logits as logits again.  At GPT-2 vocab this is one read
+// and one write of 100 KB per row, i.e. HBM-bound at ~2 * M * Vp * 2 bytes.
+#include "common.h"
+#include "kernels.h"
+
+namespace llmt {
+namespace {
+
+constexpr int kCeThreads = 512;
+constexpr int kCeWaves = kCeThreads / 64;
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+__device__ __forceinline__ float scalar_f(bf16_raw v) { return bf2f(v); }
+__device__ __forceinline__ float scalar_f(float v) { return v; }
+
+template <typename T>
+struct Vec8;
+template <>
+struct Vec8<bf16_raw> {
+  ushort8_t v;
+  __device__ void load(const bf16_raw* p) { v = *reinterpret_cast<const ushort8_t*>(p); }
+  __device__ float get(int i) const { return bf2f(v[i]); }
+  __device__ void set(int i, float f) { v[i] = f2bf(f); }
+  __device__ void store(bf16_raw* p) const { *reinterpret_cast<ushort8_t*>(p) = v; }
+};
+template <>
+struct Vec8<float> {
+  float4_t a, b;
+  __device__ void load(const float* p) {
+    a = reinterpret_cast<const float4_t*>(p)[0];
+    b = reinterpret_cast<const float4_t*>(p)[1];
+  }
+  __device__ float get(int i) const { return i < 4 ? a[i] : b[i - 4]; }
+  __device__ void set(int i, float f) {
+    if (i < 4) a[i] = f; else b[i - 4] = f;
+  }
+  __device__ void store(float* p) const {
+    reinterpret_cast<float4_t*>(p)[0] = a;
+    reinterpret_cast<float4_t*>(p)[1] = b;
+  }
+};
+
+template <int MAXV, typename T>
+__global__ __launch_bounds__(kCeThreads) void ce_fwd_bwd_kernel(
+    T* __restrict__ logits, const int64_t* __restrict__ labels, const float* __restrict__ row_w,
+    float* __restrict__ loss, int Vp, int V) {
+  __shared__ float scratch[kCeWaves];
+  const long row = blockIdx.x;
+  T* z = logits + row * (long)Vp;
+  const int nvec = Vp >> 3;
+  const int64_t label = labels[row];
+  const bool valid = label >= 0 && label < V;
+  const float t_label = valid ? scalar_f(z[label]) * kLog2e : 0.f;  // read before any write
+
+  Vec8<T> v[MAXV];
+  float m = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = threadIdx.x + j * kCeThreads;
+    if (c < nvec) {
+      v[j].load(z + 8 * c);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (8 * c + i < V) m = fmaxf(m, v[j].get(i));
+    }
+  }
+  const float zmax = block_max<kCeWaves>(m, scratch);
+  const float tmax = zmax * kLog2e;
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = threadIdx.x + j * kCeThreads;
+    if (c < nvec) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (8 * c + i < V) s += exp2f(v[j].get(i) * kLog2e - tmax);
+    }
+  }
+  const float ssum = block_sum<kCeWaves>(s, scratch);
+  const float lse2 = tmax + log2f(ssum);
+  const float w = valid ? row_w[row] : 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = threadIdx.x + j * kCeThreads;
+    if (c < nvec) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int col = 8 * c + i;
+        float gval = 0.f;
+        if (col < V) {
+          gval = exp2f(v[j].get(i) * kLog2e - lse2);
+          if (col == label) gval -= 1.f;
+          gval *= w;
+        }
+        v[j].set(i, gval);
+      }
+      v[j].store(z + 8 * c);
+    }
+  }
+  if (threadIdx.x == 0) loss[row] = valid ? (lse2 - t_label) * kLn2 : 0.f;
+}
+
+template <typename T>
+hipError_t launch_t(T* logits, const int64_t* labels, const float* row_w, float* loss, int M,
+                    int Vp, int V, hipStream_t st) {
+  const int nvec = Vp / 8;
+  const int maxv = (nvec + kCeThreads - 1) / kCeThreads;
+  dim3 grid(M), block(kCeThreads);
+#define CE_CASE(N)                                                                               \
+  case N:                                                                                        \
+    hipLaunchKernelGGL((ce_fwd_bwd_kernel<N, T>), grid, block, 0, st, logits, labels, row_w, loss, \
+                       Vp, V);                                                                   \
+    break;
+  switch (maxv) {
+    CE_CASE(1) CE_CASE(2) CE_CASE(4) CE_CASE(8) CE_CASE(13) CE_CASE(16) CE_CASE(26) CE_CASE(32)
+    default: {
+      // round up to the next instantiated size
+      if (maxv <= 4) { hipLaunchKernelGGL((ce_fwd_bwd_kernel<4, T>), grid, block, 0, st, logits, labels, row_w, loss, Vp, V); }
+      else if (maxv <= 8) { hipLaunchKernelGGL((ce_fwd_bwd_kernel<8, T>), grid, block, 0, st, logits, labels, row_w, loss, Vp, V); }
+      else if (maxv <= 13) { hipLaunchKernelGGL((ce_fwd_bwd_kernel<13, T>), grid, block, 0, st, logits, labels, row_w, loss, Vp, V); }
+      else if (maxv <= 16) { hipLaunchKernelGGL((ce_fwd_bwd_kernel<16, T>), grid, block, 0, st, logits, labels, row_w, loss, Vp, V); }
+      else if (maxv <= 26) { hipLaunchKernelGGL((ce_fwd_bwd_kernel<26, T>), grid, block, 0, st, logits, labels, row_w, loss, Vp, V); }
+      else if (maxv <= 32) { hipLaunchKernelGGL((ce_fwd_bwd_kernel<32, T>), grid, block, 0, st, logits, labels, row_w, loss, Vp, V); }
+      else return hipErrorInvalidValue;  // Vp > 131072
+    }
+  }
+#undef CE_CASE
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_cross_entropy_fwd_bwd(void* logits, bool bf16, const int64_t* labels,
+                                        const float* row_weight, float* loss, int M, int Vp,
+                                        int V, hipStream_t stream) {
+  if (Vp % 8 != 0 || V > Vp || M <= 0) return hipErrorInvalidValue;
+  if (bf16) return launch_t((bf16_raw*)logits, labels, row_weight, loss, M, Vp, V, stream);
+  return launch_t((float*)logits, labels, row_weight, loss, M, Vp, V, stream);
+}
+
+}  // namespace llmt

@@ -1,0 +1,205 @@
+// Memory-bound kernels of the fused GPT step (gfx950): exact-erf GELU forward/backward with the
+// fc-bias gradient fused in, bias-gradient column sums, token+position embedding forward and
+// backward.  Every global access is a 16-byte vector per lane (Guideline 13).
+//
+// Reference call sites: models/gpt.py:94-95/:102-103 (nn.GELU, exact erf), :176-179 (token and
+// position embeddings; gradient of the tied [V, d] table), Linear bias gradients.
+#include "common.h"
+#include "kernels.h"
+
+namespace llmt {
+namespace {
+
+constexpr float kInvSqrt2 = 0.70710678118654752f;
+constexpr float kInvSqrt2Pi = 0.39894228040143268f;
+
+__device__ __forceinline__ float gelu(float u) { return 0.5f * u * (1.f + erff(u * kInvSqrt2)); }
+__device__ __forceinline__ float gelu_grad(float u) {
+  return 0.5f * (1.f + erff(u * kInvSqrt2)) + u * kInvSqrt2Pi * __expf(-0.5f * u * u);
+}
+
+// 8-wide load/store of either dtype as f32
+template <bool BF16>
+__device__ __forceinline__ void ld8(const void* base, long i8, float* f) {
+  if (BF16) {
+    unpack8(reinterpret_cast<const ushort8_t*>(base)[i8], f);
+  } else {
+    const float4_t* p = reinterpret_cast<const float4_t*>(base) + 2 * i8;
+    float4_t a = p[0], b = p[1];
+    f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3];
+    f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
+  }
+}
+template <bool BF16>
+__device__ __forceinline__ void st8(void* base, long i8, const float* f) {
+  if (BF16) {
+    reinterpret_cast<ushort8_t*>(base)[i8] = pack8(f);
+  } else {
+    float4_t* p = reinterpret_cast<float4_t*>(base) + 2 * i8;
+    p[0] = float4_t{f[0], f[1], f[2], f[3]};
+    p[1] = float4_t{f[4], f[5], f[6], f[7]};
+  }
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(256) void gelu_fwd_kernel(const void* __restrict__ u, void* __restrict__ g,
+                                                       long n8) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float f[8];
+    ld8<BF16>(u, i, f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = gelu(f[k]);
+    st8<BF16>(g, i, f);
+  }
+}
+
+// Column-tiled [M, F] pass: a workgroup owns 64 column-vectors (512 columns) and a strip of rows;
+// its 4 waves split the strip, keep 8 f32 column partials per lane, reduce through LDS and add
+// one f32 atomic per column.  OP 0 = gelu backward (+ optional dbias), OP 1 = column sum only.
+template <int OP, bool BF16>
+__global__ __launch_bounds__(256) void colwise_kernel(const void* __restrict__ a, const void* __restrict__ u,
+                                                      void* __restrict__ out, float* __restrict__ colsum,
+                                                      int M, int F8, int rows_per_block) {
+  __shared__ float part[4][64 * 8 + 4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int cv = blockIdx.x * 64 + lane;  // column-vector index
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (cv < F8) {
+    for (int r = r0 + wid; r < r1; r += 4) {
+      const long i8 = (long)r * F8 + cv;
+      float x[8];
+      ld8<BF16>(a, i8, x);
+      if (OP == 0) {
+        float uu[8];
+        ld8<BF16>(u, i8, uu);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] *= gelu_grad(uu[k]);
+        if (BF16) {  // round first so dbias sums exactly what the next GEMM consumes
+#pragma unroll
+          for (int k = 0; k < 8; ++k) x[k] = bf2f(f2bf(x[k]));
+        }
+        st8<BF16>(out, i8, x);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += x[k];
+    }
+  }
+  if (colsum == nullptr) return;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) part[wid][lane * 8 + k] = acc[k];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 8; i += 256) {
+    const int col = blockIdx.x * 512 + i;
+    if (col < F8 * 8) atomicAdd(colsum + col, part[0][i] + part[1][i] + part[2][i] + part[3][i]);
+  }
+}
+
+// one wave per token row; float4 chunks
+__global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __restrict__ ids,
+                                                            const float* __restrict__ wte,
+                                                            const float* __restrict__ wpe,
+                                                            float* __restrict__ x, int M, int T,
+                                                            int d, int V) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int lane = threadIdx.x & 63;
+  long tok = ids[row];
+  tok = tok < 0 ? 0 : (tok >= V ? V - 1 : tok);  // clamp: never read out of bounds
+  const int t = (int)(row % T);
+  const float4_t* e = reinterpret_cast<const float4_t*>(wte + tok * (long)d);
+  const float4_t* p = reinterpret_cast<const float4_t*>(wpe + (long)t * d);
+  float4_t* o = reinterpret_cast<float4_t*>(x + row * (long)d);
+  for (int c = lane; c < (d >> 2); c += 64) o[c] = e[c] + p[c];
+}
+
+// dwte[ids[row]] += dx[row]: each wave adds one contiguous row (256-B wave segments, the
+// full-rate atomic shape on MI355X).
+__global__ __launch_bounds__(256) void embedding_bwd_tok_kernel(const float* __restrict__ dx,
+                                                                const int64_t* __restrict__ ids,
+                                                                float* __restrict__ dwte, int M,
+                                                                int d, int V) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int lane = threadIdx.x & 63;
+  const long tok = ids[row];
+  if (tok < 0 || tok >= V) return;
+  const float* src = dx + row * (long)d;
+  float* dst = dwte + tok * (long)d;
+  for (int c = lane; c < d; c += 64) atomicAdd(dst + c, src[c]);
+}
+
+// dwpe[t] += sum_b dx[b, t]: one thread per (t, float4 column chunk), no atomics.
+__global__ __launch_bounds__(256) void embedding_bwd_pos_kernel(const float* __restrict__ dx,
+                                                                float* __restrict__ dwpe, int B,
+                                                                int T, int d) {
+  const int d4 = d >> 2;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)T * d4) return;
+  const int t = (int)(idx / d4), c = (int)(idx % d4);
+  float4_t acc = {0.f, 0.f, 0.f, 0.f};
+  for (int b = 0; b < B; ++b)
+    acc += reinterpret_cast<const float4_t*>(dx + ((long)b * T + t) * d)[c];
+  reinterpret_cast<float4_t*>(dwpe + (long)t * d)[c] += acc;
+}
+
+int rows_per_block_for(int M) {
+  // ~128 row strips keep the atomic count low while giving 6-13 x 128 workgroups for F=768-3072
+  int rpb = (M + 127) / 128;
+  return rpb < 4 ? 4 : rpb;
+}
+
+}  // namespace
+
+hipError_t launch_gelu_fwd(const void* u, void* g, bool bf16, long long n, hipStream_t stream) {
+  if (n % 8 != 0) return hipErrorInvalidValue;
+  const long n8 = n / 8;
+  const int grid = stride_grid(n8, 256, 256 * 16);
+  if (bf16) hipLaunchKernelGGL(gelu_fwd_kernel<true>, dim3(grid), dim3(256), 0, stream, u, g, n8);
+  else hipLaunchKernelGGL(gelu_fwd_kernel<false>, dim3(grid), dim3(256), 0, stream, u, g, n8);
+  return hipGetLastError();
+}
+
+hipError_t launch_gelu_bwd(const void* dg, const void* u, void* du, float* dbias, bool bf16, int M,
+                           int F, hipStream_t stream) {
+  if (F % 8 != 0) return hipErrorInvalidValue;
+  const int F8 = F / 8, rpb = rows_per_block_for(M);
+  dim3 grid((F8 + 63) / 64, (M + rpb - 1) / rpb);
+  if (bf16)
+    hipLaunchKernelGGL((colwise_kernel<0, true>), grid, dim3(256), 0, stream, dg, u, du, dbias, M, F8, rpb);
+  else
+    hipLaunchKernelGGL((colwise_kernel<0, false>), grid, dim3(256), 0, stream, dg, u, du, dbias, M, F8, rpb);
+  return hipGetLastError();
+}
+
+hipError_t launch_colsum_accum(const void* dy, bool bf16, float* out, int M, int N, hipStream_t stream) {
+  if (N % 8 != 0) return hipErrorInvalidValue;
+  const int N8 = N / 8, rpb = rows_per_block_for(M);
+  dim3 grid((N8 + 63) / 64, (M + rpb - 1) / rpb);
+  if (bf16)
+    hipLaunchKernelGGL((colwise_kernel<1, true>), grid, dim3(256), 0, stream, dy, nullptr, nullptr, out, M, N8, rpb);
+  else
+    hipLaunchKernelGGL((colwise_kernel<1, false>), grid, dim3(256), 0, stream, dy, nullptr, nullptr, out, M, N8, rpb);
+  return hipGetLastError();
+}
+
+hipError_t launch_embedding_fwd(const int64_t* ids, const float* wte, const float* wpe, float* x, int B,
+                                int T, int d, int V, hipStream_t stream) {
+  if (d % 4 != 0) return hipErrorInvalidValue;
+  const int M = B * T;
+  hipLaunchKernelGGL(embedding_fwd_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, ids, wte, wpe, x, M, T, d, V);
+  return hipGetLastError();
+}
+
+hipError_t launch_embedding_bwd(const float* dx, const int64_t* ids, float* dwte, float* dwpe, int B, int T,
+                                int d, int V, hipStream_t stream) {
+  if (d % 4 != 0) return hipErrorInvalidValue;
+  const int M = B * T;
+  hipLaunchKernelGGL(embedding_bwd_tok_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, dx, ids, dwte, M, d, V);
+  const long work = (long)T * (d / 4);
+  hipLaunchKernelGGL(embedding_bwd_pos_kernel, dim3((work + 255) / 256), dim3(256), 0, stream, dx, dwpe, B, T, d);
+  return hipGetLastError();
+}
+
+}  // namespace llmt

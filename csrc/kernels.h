@@ -1,0 +1,99 @@
+// Host-side launch API of the llmtrain gfx950 kernels.
+//
+// The .hip translation units include only the HIP runtime; csrc/bindings.cpp (the only TU that
+// sees torch headers) validates tensors and calls these launchers with raw device pointers and
+// the current HIP stream.  All launchers are asynchronous and graph-capture safe (no
+// allocation, no synchronisation).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace llmt {
+
+// ---- LayerNorm --------------------------------------------------------------------------
+struct LnFwdArgs {
+  const float* x;      // [M, d] residual stream
+  const void* delta;   // [M, d] optional update added to x (bf16 or f32)
+  bool delta_bf16;
+  const float* w;
+  const float* b;
+  float* xs_out;       // [M, d] x + delta (only written when delta != nullptr)
+  void* y;             // [M, d] normalised output (bf16 or f32)
+  bool y_bf16;
+  float* mean;         // [M]
+  float* rstd;         // [M]
+  int M, d;
+  float eps;
+};
+hipError_t launch_add_layernorm_fwd(const LnFwdArgs& a, hipStream_t stream);
+
+struct LnBwdArgs {
+  const void* dy;      // [M, d] (bf16 or f32)
+  bool dy_bf16;
+  const float* xs;
+  const float* mean;
+  const float* rstd;
+  const float* w;
+  const float* dresid;   // optional [M, d] gradient added to dx
+  const float* dy_scale; // optional device scalar multiplying dy
+  float* dx;             // [M, d]
+  void* dx_lp;           // optional [M, d] copy of dx in dy's dtype
+  float* dw;             // [d] accumulated
+  float* db;             // [d] accumulated
+  float* dproj;          // optional [d] accumulated column sum of dx
+  int M, d;
+};
+hipError_t launch_layernorm_bwd(const LnBwdArgs& a, hipStream_t stream);
+
+// ---- softmax cross-entropy (forward + in-place gradient) --------------------------------
+// logits [M, Vp] bf16 (or f32), labels [M] int64, row_weight [M] f32 -> loss [M] f32;
+// logits are overwritten with (softmax - onehot) * row_weight (0 beyond column V).
+hipError_t launch_cross_entropy_fwd_bwd(void* logits, bool bf16, const int64_t* labels,
+                                        const float* row_weight, float* loss, int M, int Vp,
+                                        int V, hipStream_t stream);
+
+// ---- elementwise / reductions -----------------------------------------------------------
+hipError_t launch_gelu_fwd(const void* u, void* g, bool bf16, long long n, hipStream_t stream);
+// du = dg * gelu'(u); dbias (optional, [F]) += colsum(du); tensors are [M, F]
+hipError_t launch_gelu_bwd(const void* dg, const void* u, void* du, float* dbias, bool bf16,
+                           int M, int F, hipStream_t stream);
+// out[N] += colsum(dy[M, N])
+hipError_t launch_colsum_accum(const void* dy, bool bf16, float* out, int M, int N,
+                               hipStream_t stream);
+// x[b*T+t] = wte[ids] + wpe[t]
+hipError_t launch_embedding_fwd(const int64_t* ids, const float* wte, const float* wpe, float* x,
+                                int B, int T, int d, int V, hipStream_t stream);
+hipError_t launch_embedding_bwd(const float* dx, const int64_t* ids, float* dwte, float* dwpe,
+                                int B, int T, int d, int V, hipStream_t stream);
+
+// ---- optimizer ---------------------------------------------------------------------------
+struct AdamWArgs {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  void* shadow;          // optional compute copy (bf16 or f32), first n elements written
+  bool shadow_bf16;
+  const float* grad_scale;  // optional device scalar
+  long long n;
+  float lr, beta1, beta2, eps, weight_decay;
+  float bias_correction1, bias_correction2_sqrt;
+};
+hipError_t launch_adamw_flat(const AdamWArgs& a, hipStream_t stream);
+// out (device scalar) = sum(x^2); `partials` must hold kSumsqBlocks floats
+constexpr int kSumsqBlocks = 1024;
+hipError_t launch_sumsq(const float* x, long long n, float* partials, float* out,
+                        hipStream_t stream);
+
+// ---- causal flash attention (head_dim 64) ----------------------------------------------
+// qkv [B, T, 3, H, 64] bf16 (the packed projection output), out [B, T, H, 64] bf16,
+// lse [B, H, T] f32 (natural-log normaliser).
+hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H,
+                           hipStream_t stream);
+// dqkv [B, T, 3, H, 64] bf16; `delta` [B, H, T] f32 and `dq_accum` [B, T, H, 64] f32 scratch
+hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse,
+                           void* dqkv, float* delta, float* dq_accum, int B, int T, int H,
+                           hipStream_t stream);
+
+}  // namespace llmt

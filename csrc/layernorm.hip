@@ -1,0 +1,233 @@
+// Fused residual-add + LayerNorm forward and LayerNorm backward for gfx950.
+//
+// Replaces reference call sites models/gpt.py:86 (ln_1), :93 (ln_2), :142 (ln_f) and the
+// residual adds at :100/:104-105.  One wave64 owns one row of width d; each lane keeps its
+// ceil(d / 256) float4 chunks of the row in registers, so the statistics need no second read
+// (mean and variance are two in-register passes).  Memory bound: the kernels move 12 B/elem
+// (forward: x f32 + delta bf16 in, x' f32 + y bf16 out) and 16 B/elem (backward).
+//
+// Backward accumulates dgamma/dbeta (and optionally the column sum of dx, which is the bias
+// gradient of the projection whose output was added into this residual stream) with per-lane
+// register partials over a grid-stride run of rows, a cross-wave LDS reduction, then one fp32
+// atomic per column per workgroup.
+#include "common.h"
+#include "kernels.h"
+
+namespace llmt {
+namespace {
+
+template <typename T>
+__device__ __forceinline__ float4_t load4(const T* p);
+template <>
+__device__ __forceinline__ float4_t load4<float>(const float* p) {
+  return *reinterpret_cast<const float4_t*>(p);
+}
+template <>
+__device__ __forceinline__ float4_t load4<bf16_raw>(const bf16_raw* p) {
+  ushort4_t v = *reinterpret_cast<const ushort4_t*>(p);
+  return float4_t{bf2f(v[0]), bf2f(v[1]), bf2f(v[2]), bf2f(v[3])};
+}
+
+template <typename T>
+__device__ __forceinline__ void store4(T* p, float4_t v);
+template <>
+__device__ __forceinline__ void store4<float>(float* p, float4_t v) {
+  *reinterpret_cast<float4_t*>(p) = v;
+}
+template <>
+__device__ __forceinline__ void store4<bf16_raw>(bf16_raw* p, float4_t v) {
+  ushort4_t o;
+  o[0] = f2bf(v[0]); o[1] = f2bf(v[1]); o[2] = f2bf(v[2]); o[3] = f2bf(v[3]);
+  *reinterpret_cast<ushort4_t*>(p) = o;
+}
+
+constexpr int kLnWaves = 4;  // rows per workgroup in the forward
+
+// MAXC = max float4 chunks per lane = ceil(d / 4 / 64)
+template <int MAXC, typename TD, typename TY>
+__global__ __launch_bounds__(256) void add_ln_fwd_kernel(
+    const float* __restrict__ x, const TD* __restrict__ delta, const float* __restrict__ w,
+    const float* __restrict__ b, float* __restrict__ xs_out, TY* __restrict__ y,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out, int M, int d, float eps) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * kLnWaves + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nc = d >> 2;
+  const float* xr = x + row * d;
+  float4_t v[MAXC];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int c = lane + j * 64;
+    if (c < nc) {
+      v[j] = load4(xr + 4 * c);
+      if (delta != nullptr) {
+        v[j] += load4(delta + row * d + 4 * c);
+        store4(xs_out + row * d + 4 * c, v[j]);
+      }
+      s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
+    }
+  }
+  const float inv_d = 1.f / (float)d;
+  const float mu = wave_sum(s) * inv_d;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int c = lane + j * 64;
+    if (c < nc) {
+      float4_t t = v[j] - mu;
+      q += t[0] * t[0] + t[1] * t[1] + t[2] * t[2] + t[3] * t[3];
+    }
+  }
+  const float rs = rsqrtf(wave_sum(q) * inv_d + eps);
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int c = lane + j * 64;
+    if (c < nc) {
+      float4_t ww = load4(w + 4 * c), bb = load4(b + 4 * c);
+      store4(y + row * d + 4 * c, (v[j] - mu) * rs * ww + bb);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mu;
+    rstd_out[row] = rs;
+  }
+}
+
+constexpr int kBwdWaves = 4;
+
+template <int MAXC, typename TDY, bool LOWP_OUT>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(
+    const TDY* __restrict__ dy, const float* __restrict__ xs, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const float* __restrict__ w, const float* __restrict__ dresid,
+    const float* __restrict__ dy_scale, float* __restrict__ dx, TDY* __restrict__ dx_lp,
+    float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dproj, int M, int d) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // [kBwdWaves][3][d]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nc = d >> 2;
+  const float scale = dy_scale != nullptr ? *dy_scale : 1.f;
+  const float inv_d = 1.f / (float)d;
+
+  float4_t pw[MAXC], pb[MAXC], pp[MAXC];
+  float4_t wv[MAXC];
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    pw[j] = 0.f; pb[j] = 0.f; pp[j] = 0.f;
+    const int c = lane + j * 64;
+    wv[j] = c < nc ? load4(w + 4 * c) : float4_t{0.f, 0.f, 0.f, 0.f};
+  }
+
+  const long stride = (long)gridDim.x * kBwdWaves;
+  for (long row = (long)blockIdx.x * kBwdWaves + wid; row < M; row += stride) {
+    const float mu = mean[row], rs = rstd[row];
+    float4_t g[MAXC], xh[MAXC];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = lane + j * 64;
+      if (c < nc) {
+        g[j] = load4(dy + row * d + 4 * c) * scale;
+        xh[j] = (load4(xs + row * d + 4 * c) - mu) * rs;
+        float4_t gw = g[j] * wv[j];
+        s1 += gw[0] + gw[1] + gw[2] + gw[3];
+        float4_t gx = gw * xh[j];
+        s2 += gx[0] + gx[1] + gx[2] + gx[3];
+      }
+    }
+    const float c1 = wave_sum(s1) * inv_d, c2 = wave_sum(s2) * inv_d;
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = lane + j * 64;
+      if (c < nc) {
+        float4_t out = (g[j] * wv[j] - c1 - xh[j] * c2) * rs;
+        if (dresid != nullptr) out += load4(dresid + row * d + 4 * c);
+        store4(dx + row * d + 4 * c, out);
+        if (LOWP_OUT) store4(dx_lp + row * d + 4 * c, out);
+        pw[j] += g[j] * xh[j];
+        pb[j] += g[j];
+        pp[j] += out;
+      }
+    }
+  }
+
+  // Cross-wave reduction of the column partials, then one atomic per column per workgroup.
+  const int nacc = dproj != nullptr ? 3 : 2;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int c = lane + j * 64;
+    if (c < nc) {
+      store4(smem + (wid * 3 + 0) * d + 4 * c, pw[j]);
+      store4(smem + (wid * 3 + 1) * d + 4 * c, pb[j]);
+      if (nacc == 3) store4(smem + (wid * 3 + 2) * d + 4 * c, pp[j]);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nacc * d; i += blockDim.x) {
+    const int which = i / d, col = i - which * d;
+    float acc = 0.f;
+#pragma unroll
+    for (int wv2 = 0; wv2 < kBwdWaves; ++wv2) acc += smem[(wv2 * 3 + which) * d + col];
+    float* dst = which == 0 ? dw : (which == 1 ? db : dproj);
+    atomicAdd(dst + col, acc);
+  }
+}
+
+template <int MAXC>
+void launch_fwd_c(const LnFwdArgs& a, hipStream_t st) {
+  dim3 grid((a.M + kLnWaves - 1) / kLnWaves), block(256);
+#define LN_FWD(TD, TY)                                                                        \
+  hipLaunchKernelGGL((add_ln_fwd_kernel<MAXC, TD, TY>), grid, block, 0, st, a.x,              \
+                     (const TD*)a.delta, a.w, a.b, a.xs_out, (TY*)a.y, a.mean, a.rstd, a.M, a.d, \
+                     a.eps)
+  if (a.delta_bf16) {
+    if (a.y_bf16) LN_FWD(bf16_raw, bf16_raw); else LN_FWD(bf16_raw, float);
+  } else {
+    if (a.y_bf16) LN_FWD(float, bf16_raw); else LN_FWD(float, float);
+  }
+#undef LN_FWD
+}
+
+template <int MAXC>
+void launch_bwd_c(const LnBwdArgs& a, hipStream_t st) {
+  const int grid = stride_grid((long long)(a.M + kBwdWaves - 1) / kBwdWaves, 1, 256 * 4);
+  const size_t shm = (size_t)kBwdWaves * 3 * a.d * sizeof(float);
+#define LN_BWD(TDY, LP)                                                                         \
+  hipLaunchKernelGGL((ln_bwd_kernel<MAXC, TDY, LP>), dim3(grid), dim3(256), shm, st,            \
+                     (const TDY*)a.dy, a.xs, a.mean, a.rstd, a.w, a.dresid, a.dy_scale, a.dx,    \
+                     (TDY*)a.dx_lp, a.dw, a.db, a.dproj, a.M, a.d)
+  if (a.dy_bf16) {
+    if (a.dx_lp != nullptr) LN_BWD(bf16_raw, true); else LN_BWD(bf16_raw, false);
+  } else {
+    if (a.dx_lp != nullptr) LN_BWD(float, true); else LN_BWD(float, false);
+  }
+#undef LN_BWD
+}
+
+}  // namespace
+
+#define LN_DISPATCH(FN, ARGS, ST)                      \
+  switch ((ARGS.d / 4 + 63) / 64) {                    \
+    case 1: FN<1>(ARGS, ST); break;                    \
+    case 2: FN<2>(ARGS, ST); break;                    \
+    case 3: FN<3>(ARGS, ST); break;                    \
+    case 4: FN<4>(ARGS, ST); break;                    \
+    case 5: FN<5>(ARGS, ST); break;                    \
+    case 6: FN<6>(ARGS, ST); break;                    \
+    case 7: FN<7>(ARGS, ST); break;                    \
+    case 8: FN<8>(ARGS, ST); break;                    \
+    default: return hipErrorInvalidValue;              \
+  }
+
+hipError_t launch_add_layernorm_fwd(const LnFwdArgs& a, hipStream_t stream) {
+  if (a.d % 4 != 0 || a.M <= 0) return hipErrorInvalidValue;
+  LN_DISPATCH(launch_fwd_c, a, stream);
+  return hipGetLastError();
+}
+
+hipError_t launch_layernorm_bwd(const LnBwdArgs& a, hipStream_t stream) {
+  if (a.d % 4 != 0 || a.M <= 0) return hipErrorInvalidValue;
+  LN_DISPATCH(launch_bwd_c, a, stream);
+  return hipGetLastError();
+}
+
+}  // namespace llmt

@@ -1,0 +1,133 @@
+"""Build the in-tree HIP extension ``llmtrain/ops/_llmtrain_hip.so`` for gfx950.
+
+    python -m llmtrain.ops.build [--jobs N] [--force] [--debug]
+
+Every ``csrc/*.hip`` kernel file is compiled by ``hipcc --offload-arch=gfx950`` into its own
+object (these TUs include only the HIP runtime, so they compile in seconds); ``csrc/bindings.cpp``
+— the only TU that includes torch headers — is compiled once; everything is linked into one
+shared object that ``torch.ops.load_library`` loads.  Objects are rebuilt only when a source or
+header is newer (incremental).  The build needs no GPU: hipcc cross-compiles for gfx950.
+
+No hipify, no CUDA sources, no multi-arch fat binaries: gfx950 (MI355X, CDNA4) only.
+"""
+
+from __future__ import annotations
+
+import argparse
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+import torch
+
+__all__ = ["build", "CSRC", "OUT"]
+
+REPO = Path(__file__).resolve().parents[2]
+CSRC = REPO / "csrc"
+OUT = Path(__file__).resolve().with_name("_llmtrain_hip.so")
+OBJDIR = REPO / "build" / "hip_obj"
+ARCH = os.environ.get("LLMTRAIN_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    return str(Path(rocm) / "bin" / "hipcc")
+
+
+def _torch_dirs() -> tuple[Path, Path]:
+    root = Path(torch.__file__).resolve().parent
+    return root / "include", root / "lib"
+
+
+def _common_flags(debug: bool) -> list[str]:
+    flags = [
+        f"--offload-arch={ARCH}",
+        "-std=c++17",
+        "-fPIC",
+        "-O1" if debug else "-O3",
+        f"-I{CSRC}",
+        "-D__HIP_PLATFORM_AMD__",
+        "-Wno-unused-result",
+    ]
+    if debug:
+        flags += ["-g", "-DLLMT_DEBUG=1"]
+    return flags
+
+
+def _torch_flags() -> list[str]:
+    inc, _ = _torch_dirs()
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return [
+        f"-I{inc}",
+        f"-I{inc / 'torch' / 'csrc' / 'api' / 'include'}",
+        f"-I{sysconfig.get_paths()['include']}",
+        "-DUSE_ROCM",
+        f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+    ]
+
+
+def _headers() -> list[Path]:
+    return sorted(CSRC.glob("*.h"))
+
+
+def _stale(obj: Path, src: Path) -> bool:
+    if not obj.exists():
+        return True
+    mtime = obj.stat().st_mtime
+    return any(p.stat().st_mtime > mtime for p in [src, *_headers(), Path(__file__)])
+
+
+def _compile(src: Path, debug: bool, force: bool) -> Path:
+    obj = OBJDIR / (src.name + (".dbg" if debug else "") + ".o")
+    if not force and not _stale(obj, src):
+        return obj
+    cmd = [_hipcc(), *_common_flags(debug)]
+    if src.suffix == ".cpp":
+        cmd += ["-x", "hip", *_torch_flags()]
+    cmd += ["-c", str(src), "-o", str(obj)]
+    proc = subprocess.run(cmd, capture_output=True, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{proc.stdout}\n{proc.stderr}")
+    return obj
+
+
+def build(*, jobs: int | None = None, force: bool = False, debug: bool = False, verbose: bool = True) -> Path:
+    """Compile every kernel for gfx950 and link the extension; returns the .so path."""
+    OBJDIR.mkdir(parents=True, exist_ok=True)
+    sources = sorted(CSRC.glob("*.hip")) + [CSRC / "bindings.cpp"]
+    jobs = jobs or min(16, os.cpu_count() or 4, len(sources))
+    with ThreadPoolExecutor(max_workers=jobs) as pool:
+        objs = list(pool.map(lambda s: _compile(s, debug, force), sources))
+    newest = max(o.stat().st_mtime for o in objs)
+    if force or not OUT.exists() or OUT.stat().st_mtime < newest:
+        _, lib = _torch_dirs()
+        cmd = [
+            _hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), f"-L{lib}",
+            "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-lc10", "-lc10_hip",
+            f"-Wl,-rpath,{lib}", "-o", str(OUT),
+        ]
+        proc = subprocess.run(cmd, capture_output=True, text=True)
+        if proc.returncode != 0:
+            raise RuntimeError(f"link failed:\n{proc.stdout}\n{proc.stderr}")
+        if verbose:
+            print(f"[llmtrain.ops.build] linked {OUT} ({OUT.stat().st_size / 2**20:.1f} MiB, {ARCH})")
+    elif verbose:
+        print(f"[llmtrain.ops.build] {OUT} up to date")
+    return OUT
+
+
+def main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--jobs", type=int, default=None)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--debug", action="store_true")
+    args = ap.parse_args(argv)
+    build(jobs=args.jobs, force=args.force, debug=args.debug)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -317,6 +317,31 @@ class Trainer:
             self._optimizer.step()
         self._scheduler.step()
 
+    def batch_stream(self) -> _Batches:
+        """Endless iterator over this trainer's training DataLoader."""
+        return _Batches(self._train_loader)
+
+    def train_step(self, batches: _Batches) -> tuple[torch.Tensor, int]:
+        """One optimizer step (all micro-batches, gradient sync, clip, AdamW, LR schedule).
+
+        Returns the step's mean loss as a 0-d DEVICE tensor (no host sync) and its token count.
+        ``bench.py`` times exactly this method.
+        """
+        accum = self._cfg.trainer.grad_accum_steps
+        self._optimizer.zero_grad()
+        step_loss = torch.zeros((), dtype=torch.float32, device=self._device)
+        tokens = 0
+        for micro in range(accum):
+            batch = _to_device(batches.next(), self._device)
+            tokens += batch["input_ids"].numel()
+            with self._sync_context(micro == accum - 1):
+                with self._policy.autocast():
+                    loss, metrics = self._adapter.compute_loss(self._model, batch)
+                (loss / accum).backward()
+            step_loss += _loss_tensor(loss, metrics)
+        self._optimizer_step()
+        return step_loss / accum, tokens
+
     def _check_engine_flags(self) -> None:
         engine = getattr(self._raw_model, "engine", None)
         if engine is not None and bool(engine.padding_seen.item()):
@@ -389,22 +414,9 @@ class Trainer:
         for step in range(start_step, max_steps + 1):
             if profiler is not None:
                 profiler.before_step(step)
-            self._optimizer.zero_grad()
-            step_loss_dev = torch.zeros((), dtype=torch.float32, device=self._device)
-            step_tokens = 0
-            for micro in range(accum):
-                batch = _to_device(batches.next(), self._device)
-                step_tokens += batch["input_ids"].numel()
-                with self._sync_context(micro == accum - 1):
-                    with self._policy.autocast():
-                        loss, metrics = self._adapter.compute_loss(self._model, batch)
-                    (loss / accum).backward()
-                step_loss_dev += _loss_tensor(loss, metrics)
-            self._optimizer_step()
+            step_loss_dev, step_tokens = self.train_step(batches)
             if fail_at is not None and step == int(fail_at):
                 raise RuntimeError(f"fault injection: trainer.extra.fail_at_step={fail_at}")
-
-            step_loss_dev /= accum
             last_step_loss_dev = step_loss_dev
             tokens_local_total += step_tokens
             if step == 1:

@@ -1,0 +1,56 @@
+"""Shared test configuration.
+
+Markers: ``gpu`` (needs a MI355X; the driver runs ``-m gpu`` on a real box and ``-m "not gpu"``
+here), ``slow`` (multi-process / long running).
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+
+
+def pytest_configure(config: pytest.Config) -> None:
+    config.addinivalue_line("markers", "gpu: requires an AMD Instinct MI355X (gfx950) GPU")
+    config.addinivalue_line("markers", "slow: multi-process or long-running test")
+
+
+def minimal_payload(**overrides: object) -> dict[str, object]:
+    payload: dict[str, object] = {
+        "schema_version": 1,
+        "run": {"name": "test-run"},
+        "model": {"name": "dummy_gpt"},
+        "data": {"name": "dummy_text"},
+        "trainer": {"max_steps": 5, "warmup_steps": 0, "micro_batch_size": 1, "grad_accum_steps": 1},
+        "ddp": {},
+        "mlflow": {"enabled": False},
+        "logging": {"log_to_file": False},
+        "output": {"root_dir": "runs"},
+    }
+    payload.update(overrides)
+    return payload
+
+
+@pytest.fixture
+def in_tmp(tmp_path: Path, monkeypatch: pytest.MonkeyPatch) -> Path:
+    monkeypatch.chdir(tmp_path)
+    return tmp_path
+
+
+@pytest.fixture(scope="session")
+def gpu_device():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    from llmtrain.ops import _ext
+
+    _ext.require()  # a GPU box without the built extension is a failure, not a skip
+    return torch.device("cuda", 0)

@@ -1,0 +1,85 @@
+"""End-to-end checks of the fused MI355X GPT engine on the GPU: parity of the bf16 fused path
+(HIP kernels + hipBLASLt GEMMs + hand-written backward) against the fp32 module path, and a
+short real training run through the Trainer."""
+
+from __future__ import annotations
+
+import copy
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from llmtrain.config.schemas import RunConfig
+from llmtrain.models.gpt import GPT
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(dev, **kw):
+    torch.manual_seed(0)
+    args = dict(vocab_size=1000, block_size=256, d_model=256, n_layers=2, n_heads=4, d_ff=1024, dropout=0.0)
+    args.update(kw)
+    return GPT(**args).to(dev)
+
+
+def test_fused_matches_module_path(gpu_device):
+    ref_model = _model(gpu_device)
+    fused = copy.deepcopy(ref_model)
+    engine = fused.prepare_runtime(compute_dtype=torch.bfloat16)
+    ids = torch.randint(0, 1000, (4, 256), device=gpu_device)
+    labels = torch.randint(0, 1000, (4, 256), device=gpu_device)
+
+    logits = ref_model(ids)
+    loss_ref = F.cross_entropy(logits.reshape(-1, 1000), labels.reshape(-1))
+    (loss_ref * 0.5).backward()
+
+    engine.store.zero_grad()
+    loss = fused.fused_loss(ids, labels)
+    (loss * 0.5).backward()
+    assert abs(loss.item() - loss_ref.item()) < 2e-2
+
+    worst = 0.0
+    for (name, p), (_, q) in zip(fused.named_parameters(), ref_model.named_parameters()):
+        num = (p.grad - q.grad).norm().item()
+        den = q.grad.norm().item() + 1e-12
+        worst = max(worst, num / den)
+        assert num / den < 5e-2, f"{name}: relative grad error {num / den:.3e}"
+    print("worst relative grad error", worst)
+
+
+def test_fused_no_grad_eval_matches(gpu_device):
+    model = _model(gpu_device)
+    model.prepare_runtime(compute_dtype=torch.bfloat16)
+    ids = torch.randint(0, 1000, (2, 256), device=gpu_device)
+    with torch.no_grad():
+        fused_loss = model.fused_loss(ids, ids).item()
+        ref_loss = F.cross_entropy(model(ids).reshape(-1, 1000), ids.reshape(-1)).item()
+    assert abs(fused_loss - ref_loss) < 2e-2
+
+
+def test_trainer_fused_gpu_learns(gpu_device, in_tmp):
+    cfg = RunConfig.model_validate(
+        {
+            "schema_version": 1,
+            "run": {"name": "gpu-fused", "device": "cuda", "precision": "bf16", "seed": 3},
+            "model": {"name": "gpt", "vocab_size": 512, "block_size": 128, "d_model": 128, "n_layers": 2,
+                      "n_heads": 2, "d_ff": 512, "dropout": 0.0},
+            "data": {"name": "synthetic_tokens", "num_workers": 0,
+                     "extra": {"train_sequences": 512, "val_sequences": 32, "branching": 2}},
+            "trainer": {"max_steps": 60, "micro_batch_size": 16, "grad_accum_steps": 2, "lr": 3e-3,
+                        "warmup_steps": 5, "log_every_steps": 20, "eval_every_steps": 60, "save_every_steps": 60},
+            "ddp": {}, "mlflow": {"enabled": False}, "logging": {"log_to_file": False},
+            "output": {"root_dir": "runs"},
+        }
+    )
+    from llmtrain.training.trainer import Trainer
+
+    trainer = Trainer(cfg)
+    assert trainer.model.engine is not None  # fused path active
+    result = trainer.fit()
+    assert math.isfinite(result.final_loss)
+    assert result.first_step_loss is not None and result.final_loss < result.first_step_loss - 1.0
+    assert result.final_val_loss is not None and result.final_val_loss < math.log(512)
+    assert result.peak_memory > 0.0

@@ -1,0 +1,193 @@
+"""Numerics of every gfx950 HIP kernel against the plain-PyTorch fp32 oracle of the same op
+(``llmtrain.ops.reference``).  Inputs are random (never zero-filled) and shapes cover both the
+GPT-2 124M production sizes and ragged/small edge cases."""
+
+from __future__ import annotations
+
+import math
+
+import pytest
+import torch
+
+from llmtrain.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def hip():
+    return torch.ops.llmtrain_hip
+
+
+def _close(a, b, atol, rtol, what=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{what}: {bad} elements out of tolerance, max err {err.max().item():.3e}"
+
+
+@pytest.mark.parametrize("M,d", [(4096, 768), (37, 64), (513, 1600)])
+@pytest.mark.parametrize("with_delta", [False, True])
+def test_add_layernorm_fwd(gpu_device, M, d, with_delta):
+    g = torch.Generator(device="cpu").manual_seed(M + d)
+    x = torch.randn(M, d, generator=g).to(gpu_device)
+    delta = torch.randn(M, d, generator=g).to(gpu_device, torch.bfloat16) if with_delta else None
+    w = (1 + 0.1 * torch.randn(d, generator=g)).to(gpu_device)
+    b = (0.1 * torch.randn(d, generator=g)).to(gpu_device)
+    xs, y, mu, rs = hip().add_layernorm_fwd(x, delta, w, b, 1e-5, torch.bfloat16)
+    xs_r, y_r, mu_r, rs_r = ref.add_layernorm_fwd(x, delta, w, b, 1e-5, torch.float32)
+    if with_delta:
+        _close(xs, xs_r, 1e-6, 1e-6, "xs")
+    _close(mu, mu_r, 1e-5, 1e-5, "mean")
+    _close(rs, rs_r, 1e-4, 1e-4, "rstd")
+    _close(y, y_r, 2e-2, 1e-2, "y(bf16)")
+
+
+@pytest.mark.parametrize("M,d", [(4096, 768), (100, 64)])
+def test_layernorm_bwd(gpu_device, M, d):
+    g = torch.Generator(device="cpu").manual_seed(7)
+    x = torch.randn(M, d, generator=g).to(gpu_device)
+    w = (1 + 0.1 * torch.randn(d, generator=g)).to(gpu_device)
+    b = torch.zeros(d).to(gpu_device)
+    _, _, mu, rs = ref.add_layernorm_fwd(x, None, w, b, 1e-5, torch.float32)
+    dy = torch.randn(M, d, generator=g).to(gpu_device, torch.bfloat16)
+    dres = torch.randn(M, d, generator=g).to(gpu_device)
+    scale = torch.tensor(0.5, device=gpu_device)
+    dw, db, dp = (torch.full((d,), 0.25, device=gpu_device) for _ in range(3))
+    dw_r, db_r, dp_r = dw.clone(), db.clone(), dp.clone()
+    dx, dx_lp = hip().layernorm_bwd(dy, x, mu, rs, w, dres, dw, db, scale, True, dp)
+    dx_r = ref.layernorm_bwd(dy, x, mu, rs, w, dres, dw_r, db_r, scale)
+    ref.colsum_accum(dx_r, dp_r)
+    _close(dx, dx_r, 1e-4, 1e-4, "dx")
+    _close(dx_lp, dx_r, 2e-2, 1e-2, "dx_lp")
+    _close(dw, dw_r, 1e-2, 1e-4, "dgamma")
+    _close(db, db_r, 1e-2, 1e-4, "dbeta")
+    _close(dp, dp_r, 2e-2, 1e-4, "dproj")
+
+
+@pytest.mark.parametrize("M,V,Vp", [(256, 50257, 50304), (64, 16, 64), (33, 1000, 1024)])
+def test_cross_entropy_fwd_bwd(gpu_device, M, V, Vp):
+    g = torch.Generator(device="cpu").manual_seed(V)
+    logits = (3 * torch.randn(M, Vp, generator=g)).to(gpu_device, torch.bfloat16)
+    labels = torch.randint(0, V, (M,), generator=g).to(gpu_device)
+    labels[3] = -100  # ignored row
+    w = torch.rand(M, generator=g).to(gpu_device) / M
+    lg_r = logits.float().clone()
+    loss_r = ref.cross_entropy_fwd_bwd(lg_r, labels, V, w)
+    lg = logits.clone()
+    loss = hip().cross_entropy_fwd_bwd(lg, labels, V, w)
+    _close(loss, loss_r, 1e-3, 1e-4, "loss")
+    _close(lg, lg_r, 1e-6, 2e-2, "dlogits")
+    assert torch.all(lg[:, V:] == 0)
+
+
+def test_gelu_fwd_bwd(gpu_device):
+    g = torch.Generator(device="cpu").manual_seed(3)
+    M, F = 2048, 3072
+    u = (2 * torch.randn(M, F, generator=g)).to(gpu_device, torch.bfloat16)
+    _close(hip().gelu_fwd(u), ref.gelu_fwd(u.float()), 1e-2, 1e-2, "gelu")
+    dg = torch.randn(M, F, generator=g).to(gpu_device, torch.bfloat16)
+    dbias = torch.zeros(F, device=gpu_device)
+    dbias_r = torch.zeros(F, device=gpu_device)
+    du = hip().gelu_bwd(dg, u, dbias)
+    du_r = ref.gelu_bwd(dg.float(), u.float(), dbias_r)
+    _close(du, du_r, 2e-2, 2e-2, "du")
+    _close(dbias, dbias_r, 0.3, 1e-2, "dbias")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_colsum(gpu_device, dtype):
+    g = torch.Generator(device="cpu").manual_seed(4)
+    dy = torch.randn(1000, 2304, generator=g).to(gpu_device, dtype)
+    out = torch.ones(2304, device=gpu_device)
+    out_r = out.clone()
+    hip().colsum_accum(dy, out)
+    ref.colsum_accum(dy, out_r)
+    _close(out, out_r, 1e-2, 1e-4, "colsum")
+
+
+def test_embedding(gpu_device):
+    g = torch.Generator(device="cpu").manual_seed(5)
+    B, T, d, V = 4, 128, 768, 5000
+    ids = torch.randint(0, V, (B, T), generator=g).to(gpu_device)
+    ids[0, :10] = 7  # repeated token: atomics must accumulate
+    wte = torch.randn(V, d, generator=g).to(gpu_device)
+    wpe = torch.randn(256, d, generator=g).to(gpu_device)
+    _close(hip().embedding_fwd(ids, wte, wpe), ref.embedding_fwd(ids, wte, wpe), 1e-6, 1e-6, "emb fwd")
+    dx = torch.randn(B * T, d, generator=g).to(gpu_device)
+    dwte, dwpe = torch.zeros_like(wte), torch.zeros_like(wpe)
+    dwte_r, dwpe_r = dwte.clone(), dwpe.clone()
+    hip().embedding_bwd(dx, ids, dwte, dwpe)
+    ref.embedding_bwd(dx, ids, dwte_r, dwpe_r)
+    _close(dwte, dwte_r, 1e-4, 1e-5, "dwte")
+    _close(dwpe, dwpe_r, 1e-4, 1e-5, "dwpe")
+
+
+def test_sumsq_and_adamw(gpu_device):
+    g = torch.Generator(device="cpu").manual_seed(6)
+    n = 1_000_003  # ragged tail
+    p = torch.randn(n, generator=g).to(gpu_device)
+    grad = torch.randn(n, generator=g).to(gpu_device)
+    m = (0.1 * torch.randn(n, generator=g)).to(gpu_device)
+    v = torch.rand(n, generator=g).to(gpu_device) * 0.01
+    s = hip().sumsq(grad)
+    assert math.isclose(float(s), float(grad.double().pow(2).sum()), rel_tol=1e-5)
+    scale = torch.tensor(0.7, device=gpu_device)
+    shadow = torch.zeros(n + 64, device=gpu_device, dtype=torch.bfloat16)
+    p_r, m_r, v_r = p.clone(), m.clone(), v.clone()
+    kw = dict(lr=3e-4, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.1, step=7)
+    hip().adamw_flat(p, grad, m, v, shadow, kw["lr"], kw["beta1"], kw["beta2"], kw["eps"], kw["weight_decay"], kw["step"], scale)
+    ref.adamw_flat(p_r, grad, m_r, v_r, None, grad_scale=scale, **kw)
+    _close(p, p_r, 1e-6, 1e-5, "param")
+    _close(m, m_r, 1e-7, 1e-5, "exp_avg")
+    _close(v, v_r, 1e-9, 1e-4, "exp_avg_sq")  # fma vs mul+add: 1 ulp-level
+    _close(shadow[:n], p_r, 1e-2, 1e-2, "shadow")
+    assert torch.all(shadow[n:] == 0)
+
+
+def test_adamw_matches_torch_adamw(gpu_device):
+    """Several steps of the fused kernel track torch.optim.AdamW (the reference optimizer)."""
+    g = torch.Generator(device="cpu").manual_seed(8)
+    p0 = torch.randn(4096, generator=g)
+    p = p0.clone().to(gpu_device)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    tp = torch.nn.Parameter(p0.clone().to(gpu_device))
+    opt = torch.optim.AdamW([tp], lr=1e-2, weight_decay=0.1)
+    for step in range(1, 6):
+        grad = torch.randn(4096, generator=g).to(gpu_device)
+        tp.grad = grad.clone()
+        opt.step()
+        hip().adamw_flat(p, grad, m, v, None, 1e-2, 0.9, 0.999, 1e-8, 0.1, step, None)
+    _close(p, tp.detach(), 1e-6, 1e-5, "adamw vs torch")
+
+
+@pytest.mark.parametrize("B,T,H", [(2, 1024, 12), (1, 256, 2), (2, 200, 3), (1, 70, 1)])
+def test_attention_fwd_bwd(gpu_device, B, T, H):
+    g = torch.Generator(device="cpu").manual_seed(B * T + H)
+    d = 64 * H
+    qkv = torch.randn(B * T, 3 * d, generator=g).to(gpu_device, torch.bfloat16)
+    out, lse = hip().attn_fwd(qkv, B, T, H)
+    out_r, lse_r = ref.attn_fwd(qkv.float(), B, T, H)
+    _close(lse, lse_r, 2e-3, 1e-3, "lse")
+    _close(out, out_r, 2e-2, 2e-2, "out")
+    dout = torch.randn(B * T, d, generator=g).to(gpu_device, torch.bfloat16)
+    dqkv = hip().attn_bwd(dout, qkv, out, lse, B, T, H)
+    dqkv_r = ref.attn_bwd(dout.float(), qkv.float(), out.float(), lse, B, T, H)
+    names = ["dq", "dk", "dv"]
+    a = dqkv.float().view(B, T, 3, H, 64)
+    r = dqkv_r.view(B, T, 3, H, 64)
+    for i, name in enumerate(names):
+        scale = r[:, :, i].abs().max().item()
+        _close(a[:, :, i], r[:, :, i], 2e-2 * scale, 3e-2, name)
+
+
+def test_attention_causality(gpu_device):
+    """Changing future tokens never changes earlier outputs (reference tests/test_gpt_model.py:11-40)."""
+    g = torch.Generator(device="cpu").manual_seed(11)
+    B, T, H = 1, 256, 2
+    qkv = torch.randn(B * T, 3 * 64 * H, generator=g).to(gpu_device, torch.bfloat16)
+    out1, _ = hip().attn_fwd(qkv, B, T, H)
+    qkv2 = qkv.clone()
+    qkv2[200:] = torch.randn(56, 3 * 64 * H, generator=g).to(gpu_device, torch.bfloat16)
+    out2, _ = hip().attn_fwd(qkv2, B, T, H)
+    assert torch.equal(out1[:200], out2[:200])

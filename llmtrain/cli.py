@@ -91,12 +91,27 @@ def _log_run_artifacts(tracker: Tracker, run_dir: Path) -> None:
             tracker.log_artifact(path, artifact_path="artifacts")
 
 
+class _StderrHandler(logging.StreamHandler):
+    """Writes to whatever ``sys.stderr`` is at emit time (robust to stream swaps in embedders)."""
+
+    def __init__(self) -> None:
+        super().__init__(sys.stderr)
+
+    @property  # type: ignore[override]
+    def stream(self) -> TextIO:
+        return sys.stderr
+
+    @stream.setter
+    def stream(self, value: TextIO) -> None:
+        pass
+
+
 def _route_to_stderr(name: str, template: logging.Logger) -> logging.Logger:
     """Send a child logger's records to stderr only (``--json`` keeps stdout clean)."""
     child = logging.getLogger(name)
     child.setLevel(template.level)
     child.handlers.clear()
-    handler = logging.StreamHandler(sys.stderr)
+    handler = _StderrHandler()
     handler.setFormatter(template.handlers[0].formatter if template.handlers else None)
     child.addHandler(handler)
     child.propagate = False

@@ -54,3 +54,30 @@ def gpu_device():
 
     _ext.require()  # a GPU box without the built extension is a failure, not a skip
     return torch.device("cuda", 0)
+
+
+class _ListHandler:
+    pass
+
+
+@pytest.fixture
+def trainer_records():
+    """Records emitted by the trainer logger, independent of how the CLI configured handlers."""
+    import logging
+
+    records: list[logging.LogRecord] = []
+
+    class Collect(logging.Handler):
+        def emit(self, record: logging.LogRecord) -> None:
+            records.append(record)
+
+    logger = logging.getLogger("llmtrain.training.trainer")
+    handler = Collect(level=logging.DEBUG)
+    old_level = logger.level
+    logger.addHandler(handler)
+    logger.setLevel(logging.INFO)
+    try:
+        yield records
+    finally:
+        logger.removeHandler(handler)
+        logger.setLevel(old_level)

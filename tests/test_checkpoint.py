@@ -3,7 +3,6 @@ plus atomic writes, safe loading of reference-style payloads and the fused path.
 
 from __future__ import annotations
 
-import logging
 import random
 from pathlib import Path
 
@@ -103,11 +102,9 @@ def test_resume_by_file_and_run_id_and_errors(tmp_path: Path, monkeypatch: pytes
     assert result.resumed_from_step == 4 and result.final_step == 4
 
 
-def test_config_mismatch_warns(tmp_path: Path, caplog: pytest.LogCaptureFixture) -> None:
+def test_config_mismatch_warns(tmp_path: Path, trainer_records) -> None:  # type: ignore[no-untyped-def]
     cfg = _cfg(tmp_path, max_steps=2)
     Trainer(cfg, run_dir=tmp_path / "run").fit()
     other = _cfg(tmp_path, max_steps=3, lr=1e-3)
-    logging.getLogger("llmtrain.training.trainer").propagate = True
-    with caplog.at_level(logging.WARNING, logger="llmtrain.training.trainer"):
-        Trainer(other).fit(resume_from=str(tmp_path / "run" / "checkpoints"))
-    assert any("config mismatch" in r.getMessage() for r in caplog.records)
+    Trainer(other).fit(resume_from=str(tmp_path / "run" / "checkpoints"))
+    assert any("config mismatch" in r.getMessage() for r in trainer_records)

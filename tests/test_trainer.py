@@ -4,7 +4,6 @@ CPU, device-side loss accumulation, fault injection, NaN guard)."""
 
 from __future__ import annotations
 
-import logging
 import math
 from unittest.mock import Mock
 
@@ -80,22 +79,17 @@ def test_lr_schedule_warmup_then_cosine() -> None:
     assert lrs[10] == 0.0
 
 
-def test_log_cadence_includes_final_step(caplog: pytest.LogCaptureFixture) -> None:
-    logger = logging.getLogger("llmtrain.training.trainer")
-    logger.propagate = True
-    with caplog.at_level(logging.INFO, logger="llmtrain.training.trainer"):
-        Trainer(_cfg(max_steps=5, log_every_steps=2)).fit()
-    steps = [r.getMessage().split()[0] for r in caplog.records if r.getMessage().startswith("step=")]
+def test_log_cadence_includes_final_step(trainer_records) -> None:  # type: ignore[no-untyped-def]
+    Trainer(_cfg(max_steps=5, log_every_steps=2)).fit()
+    steps = [r.getMessage().split()[0] for r in trainer_records if r.getMessage().startswith("step=")]
     assert steps == ["step=2/5", "step=4/5", "step=5/5"]
-    line = next(r.getMessage() for r in caplog.records if r.getMessage().startswith("step=2/5"))
+    line = next(r.getMessage() for r in trainer_records if r.getMessage().startswith("step=2/5"))
     assert "loss=" in line and "lr=" in line and "tokens_per_sec=" in line and "step_time=" in line
 
 
-def test_eval_cadence(caplog: pytest.LogCaptureFixture) -> None:
-    logging.getLogger("llmtrain.training.trainer").propagate = True
-    with caplog.at_level(logging.INFO, logger="llmtrain.training.trainer"):
-        Trainer(_cfg(max_steps=7, eval_every_steps=3)).fit()
-    evals = [r.getMessage().split()[0] for r in caplog.records if r.getMessage().startswith("val_step=")]
+def test_eval_cadence(trainer_records) -> None:  # type: ignore[no-untyped-def]
+    Trainer(_cfg(max_steps=7, eval_every_steps=3)).fit()
+    evals = [r.getMessage().split()[0] for r in trainer_records if r.getMessage().startswith("val_step=")]
     assert evals == ["val_step=3/7", "val_step=6/7", "val_step=7/7"]
 
 

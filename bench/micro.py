@@ -1,0 +1,100 @@
+"""Micro-benchmarks for kernel-level A/B on the MI355X (run on the GPU box).
+
+    python bench/micro.py gemm      # hipBLASLt variants for the GPT-2 GEMM shapes
+    python bench/micro.py attn      # llmtrain flash-attention vs torch SDPA
+"""
+
+from __future__ import annotations
+
+import json
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def timeit(fn, iters: int = 20, warmup: int = 5) -> float:
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(iters):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        torch.cuda.synchronize()
+        times.append(s.elapsed_time(e))
+    times.sort()
+    return times[len(times) // 2]  # median ms
+
+
+def gemm(M: int = 32768) -> list[dict]:
+    from llmtrain.ops import _ext
+
+    _ext.require()
+    dev = torch.device("cuda")
+    rows = []
+    shapes = {"qkv": (768, 2304), "out": (768, 768), "fc": (768, 3072), "proj": (3072, 768), "head": (768, 50304)}
+    for name, (K, N) in shapes.items():
+        x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+        w = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
+        dy = torch.randn(M, N, device=dev, dtype=torch.bfloat16)
+        flops = 2.0 * M * K * N
+        acc = torch.zeros(N, K, device=dev)
+        variants = {
+            "fwd x@w^T": lambda: torch.mm(x, w.t()),
+            "dX dy@w": lambda: torch.mm(dy, w),
+            "dW addmm f32 inplace": lambda: torch.addmm(acc, dy.t(), x, out_dtype=torch.float32, out=acc),
+            "dW mm f32 out": lambda: torch.mm(dy.t(), x, out_dtype=torch.float32),
+            "dW mm bf16": lambda: torch.mm(dy.t(), x),
+            "dW mm bf16 + add": lambda: acc.add_(torch.mm(dy.t(), x)),
+            "dW^T mm bf16 (x^T dy)": lambda: torch.mm(x.t(), dy),
+            "dW llmtrain split-K wgrad": lambda: torch.ops.llmtrain_hip.wgrad_gemm(dy, x, acc, 0),
+        }
+        for vname, fn in variants.items():
+            ms = timeit(fn)
+            rows.append({"gemm": name, "variant": vname, "ms": round(ms, 4), "TFLOPs": round(flops / ms / 1e9, 1)})
+            print(json.dumps(rows[-1]), flush=True)
+        del x, w, dy, acc
+    return rows
+
+
+def attn(B: int = 32, T: int = 1024, H: int = 12) -> list[dict]:
+    from llmtrain.ops import _ext
+
+    _ext.require()
+    ops = torch.ops.llmtrain_hip
+    dev = torch.device("cuda")
+    d = 64 * H
+    qkv = torch.randn(B * T, 3 * d, device=dev, dtype=torch.bfloat16)
+    dout = torch.randn(B * T, d, device=dev, dtype=torch.bfloat16)
+    flops_fwd = 4.0 * B * H * T * T * 64 / 2  # causal
+    rows = []
+    out, lse = ops.attn_fwd(qkv, B, T, H)
+    ms = timeit(lambda: ops.attn_fwd(qkv, B, T, H))
+    rows.append({"attn": "llmtrain fwd", "ms": round(ms, 4), "TFLOPs": round(flops_fwd / ms / 1e9, 1)})
+    ms = timeit(lambda: ops.attn_bwd(dout, qkv, out, lse, B, T, H))
+    rows.append({"attn": "llmtrain bwd", "ms": round(ms, 4), "TFLOPs": round(2.5 * flops_fwd / ms / 1e9, 1)})
+    q, k, v = (t.transpose(1, 2).contiguous() for t in qkv.view(B, T, 3, H, 64).unbind(2))
+    q.requires_grad_(True); k.requires_grad_(True); v.requires_grad_(True)
+    do = dout.view(B, T, H, 64).transpose(1, 2).contiguous()
+    f = lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=True)  # noqa: E731
+    ms = timeit(f)
+    rows.append({"attn": "torch sdpa fwd", "ms": round(ms, 4), "TFLOPs": round(flops_fwd / ms / 1e9, 1)})
+    o = f()
+    ms = timeit(lambda: torch.autograd.grad(o, (q, k, v), do, retain_graph=True))
+    rows.append({"attn": "torch sdpa bwd", "ms": round(ms, 4), "TFLOPs": round(2.5 * flops_fwd / ms / 1e9, 1)})
+    for r in rows:
+        print(json.dumps(r), flush=True)
+    return rows
+
+
+if __name__ == "__main__":
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what in ("gemm", "all"):
+        gemm()
+    if what in ("attn", "all"):
+        attn()

@@ -288,6 +288,23 @@ Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const 
   return dqkv;
 }
 
+// ---- weight-gradient GEMM --------------------------------------------------------------------
+void wgrad_gemm(const Tensor& dy, const Tensor& x, Tensor c, int64_t split) {
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && c.is_cuda(), "wgrad_gemm: GPU tensors required");
+  check_dtype(dy, at::kBFloat16, "dy");
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(c, at::kFloat, "c");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && c.dim() == 2, "wgrad_gemm: 2D operands");
+  TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1 && c.stride(1) == 1, "wgrad_gemm: unit inner stride");
+  const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
+  TORCH_CHECK(x.size(0) == M && c.size(0) == N && c.size(1) == K, "wgrad_gemm: shape mismatch");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(c.device());
+  check_hip(llmt::launch_wgrad_gemm(dy.data_ptr(), (int)dy.stride(0), x.data_ptr(), (int)x.stride(0),
+                                    c.data_ptr<float>(), (int)c.stride(0), (int)M, (int)N, (int)K, (int)split,
+                                    cur_stream()),
+            "wgrad_gemm");
+}
+
 // ---- optimizer -------------------------------------------------------------------------------
 Tensor sumsq(const Tensor& x) {
   check_gpu(x, "x");
@@ -354,6 +371,7 @@ TORCH_LIBRARY(llmtrain_hip, m) {
   m.def("embedding_bwd(Tensor dx, Tensor ids, Tensor(a!) dwte, Tensor(b!) dwpe) -> ()");
   m.def("attn_fwd(Tensor qkv, int B, int T, int H) -> (Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, int B, int T, int H) -> Tensor");
+  m.def("wgrad_gemm(Tensor dy, Tensor x, Tensor(a!) c, int split=0) -> ()");
   m.def("sumsq(Tensor x) -> Tensor");
   m.def("adamw_flat(Tensor(a!) param, Tensor grad, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor(d!)? shadow,"
         " float lr, float beta1, float beta2, float eps, float weight_decay, int step, Tensor? grad_scale) -> ()");
@@ -370,6 +388,7 @@ TORCH_LIBRARY_IMPL(llmtrain_hip, CUDA, m) {
   m.impl("embedding_bwd", &embedding_bwd);
   m.impl("attn_fwd", &attn_fwd);
   m.impl("attn_bwd", &attn_bwd);
+  m.impl("wgrad_gemm", &wgrad_gemm);
   m.impl("sumsq", &sumsq);
   m.impl("adamw_flat", &adamw_flat);
 }

@@ -86,6 +86,11 @@ constexpr int kSumsqBlocks = 1024;
 hipError_t launch_sumsq(const float* x, long long n, float* partials, float* out,
                         hipStream_t stream);
 
+// ---- weight-gradient GEMM: C[N, K] (f32) += dY[M, N]^T X[M, K] (bf16), split-K + atomics --
+// split <= 0 picks a split that yields ~2 workgroups per CU.
+hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N,
+                             int K, int split, hipStream_t stream);
+
 // ---- causal flash attention (head_dim 64) ----------------------------------------------
 // qkv [B, T, 3, H, 64] bf16 (the packed projection output), out [B, T, H, 64] bf16,
 // lse [B, H, T] f32 (natural-log normaliser).

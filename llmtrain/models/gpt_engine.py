@@ -35,6 +35,7 @@ Reference call sites replaced: ``models/gpt.py:49-74`` (attention), ``:86-105`` 
 
 from __future__ import annotations
 
+import os
 from collections.abc import Callable
 from dataclasses import dataclass, field
 from typing import Any
@@ -164,6 +165,7 @@ class FusedGPTEngine:
         self.grad_ready: Callable[[str], None] | None = None
         self.padding_seen = torch.zeros((), dtype=torch.bool, device=self.store.device)
         self._anchor = torch.zeros((), requires_grad=True, device=self.store.device)
+        self.wgrad_impl = os.environ.get("LLMTRAIN_WGRAD", "hip")
 
     # ------------------------------------------------------------------------------------
 
@@ -176,6 +178,15 @@ class FusedGPTEngine:
 
     def _g(self, p: torch.Tensor) -> torch.Tensor:
         return self.store.grad_of(p)
+
+    def _wgrad(self, dst: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
+        """Block weight gradients: the split-K MFMA kernel (``ops.wgrad_accum``) on GPU — it fills
+        the chip on these M-deep reductions where hipBLASLt picks too few tiles — unless
+        ``LLMTRAIN_WGRAD=hipblaslt`` selects the library GEMM for A/B runs."""
+        if dst.is_cuda and dy.dtype == torch.bfloat16 and self.wgrad_impl == "hip":
+            ops.wgrad_accum(dst, dy, x)
+        else:
+            accumulate_wgrad(dst, dy, x)
 
     def _linear(self, x: torch.Tensor, layer: torch.nn.Linear) -> torch.Tensor:
         w = self._w(layer.weight)
@@ -265,11 +276,11 @@ class FusedGPTEngine:
         for i in reversed(range(len(self.blocks))):
             blk, a = self.blocks[i], st.blocks[i]
             # MLP: delta = g Wp^T + bp ; dx is d(delta) (bias grad already summed by the LN bwd)
-            accumulate_wgrad(self._g(blk.mlp_proj.weight), dx_lp, a.g)
+            self._wgrad(self._g(blk.mlp_proj.weight), dx_lp, a.g)
             dg = torch.mm(dx_lp, self._w(blk.mlp_proj.weight))
             du = ops.gelu_bwd(dg, a.u, self._g(blk.mlp_fc.bias))
             del dg
-            accumulate_wgrad(self._g(blk.mlp_fc.weight), du, a.h2)
+            self._wgrad(self._g(blk.mlp_fc.weight), du, a.h2)
             dh2 = torch.mm(du, self._w(blk.mlp_fc.weight))
             del du
             dxm, dy_lp = ops.layernorm_bwd(
@@ -278,13 +289,13 @@ class FusedGPTEngine:
             )
             del dh2, dx, dx_lp
             # attention output projection
-            accumulate_wgrad(self._g(blk.attn.out_proj.weight), dy_lp, a.att)
+            self._wgrad(self._g(blk.attn.out_proj.weight), dy_lp, a.att)
             datt = torch.mm(dy_lp, self._w(blk.attn.out_proj.weight))
             del dy_lp
             dqkv = ops.attn_bwd(datt, a.qkv, a.att, a.lse, bsz, seqlen, self.n_heads)
             del datt
             ops.colsum_accum(dqkv, self._g(blk.attn.qkv_proj.bias))
-            accumulate_wgrad(self._g(blk.attn.qkv_proj.weight), dqkv, a.h1)
+            self._wgrad(self._g(blk.attn.qkv_proj.weight), dqkv, a.h1)
             dh1 = torch.mm(dqkv, self._w(blk.attn.qkv_proj.weight))
             del dqkv
             prev_bias = self._g(self.blocks[i - 1].mlp_proj.bias) if i > 0 else None

@@ -118,6 +118,15 @@ def attn_bwd(dout, qkv, out, lse, bsz: int, seqlen: int, n_heads: int):
     return ref.attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads)
 
 
+def wgrad_accum(dst, dy, x) -> None:
+    """``dst (fp32 [N, K]) += dy[M, N]^T @ x[M, K]`` — split-K MFMA GEMM with atomic fp32
+    accumulation on GPU (``dy`` may be a column slice with a larger row stride)."""
+    if _on_gpu(dst):
+        hip_ops().wgrad_gemm(dy, x, dst, 0)
+    else:
+        dst.addmm_(dy.t().float(), x.float())
+
+
 def sumsq(x):
     if _on_gpu(x):
         return hip_ops().sumsq(x)

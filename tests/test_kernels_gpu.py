@@ -191,3 +191,23 @@ def test_attention_causality(gpu_device):
     qkv2[200:] = torch.randn(56, 3 * 64 * H, generator=g).to(gpu_device, torch.bfloat16)
     out2, _ = hip().attn_fwd(qkv2, B, T, H)
     assert torch.equal(out1[:200], out2[:200])
+
+
+@pytest.mark.parametrize("M,N,K,lda", [(4096, 768, 768, 768), (2048, 2304, 768, 2304), (1000, 200, 72, 200),
+                                        (3000, 1000, 768, 1024)])
+def test_wgrad_gemm(gpu_device, M, N, K, lda):
+    """Split-K MFMA weight-gradient GEMM accumulates dY^T X into an existing fp32 buffer; also
+    with a column-slice dY (row stride lda > N, like the vocab-padded logits)."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    dy_full = torch.randn(M, lda, generator=g).to(gpu_device, torch.bfloat16)
+    dy = dy_full[:, :N]
+    x = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)
+    c = torch.randn(N, K, generator=g).to(gpu_device)
+    want = c + dy.float().t() @ x.float()
+    hip().wgrad_gemm(dy, x, c, 0)
+    scale = want.abs().max().item()
+    _close(c, want, 1e-3 * scale, 1e-3, "wgrad")
+    # an explicit split also works and is additive
+    c2 = torch.zeros(N, K, device=gpu_device)
+    hip().wgrad_gemm(dy, x, c2, 3)
+    _close(c2, dy.float().t() @ x.float(), 1e-3 * scale, 1e-3, "wgrad split=3")

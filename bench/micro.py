@@ -53,6 +53,12 @@ def gemm(M: int = 32768) -> list[dict]:
             "dW mm bf16 + add": lambda: acc.add_(torch.mm(dy.t(), x)),
             "dW^T mm bf16 (x^T dy)": lambda: torch.mm(x.t(), dy),
             "dW llmtrain split-K wgrad": lambda: torch.ops.llmtrain_hip.wgrad_gemm(dy, x, acc, 0),
+            "dW hipblaslt bmm split8 + sum": lambda: acc.add_(
+                torch.bmm(dy.view(8, M // 8, N).transpose(1, 2), x.view(8, M // 8, K)).float().sum(0)
+            ),
+            "dW hipblaslt bmm split16 + sum": lambda: acc.add_(
+                torch.bmm(dy.view(16, M // 16, N).transpose(1, 2), x.view(16, M // 16, K)).float().sum(0)
+            ),
         }
         for vname, fn in variants.items():
             ms = timeit(fn)

@@ -26,7 +26,7 @@ namespace attn {
 
 constexpr int kBwdWaves = 8;
 constexpr int kKvBlk = 32 * kBwdWaves;  // 256 keys per workgroup
-constexpr int kQTile = 32;
+constexpr int kQTile = 64;  // query rows per sweep step (two 32-row MFMA tiles)
 
 // delta[b, h, t] = sum_d dO[b, t, h, d] * O[b, t, h, d]; 8 lanes per row
 __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restrict__ dout,
@@ -74,11 +74,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
                                                           const float* __restrict__ delta,
                                                           bf16_raw* __restrict__ dqkv,
                                                           float* __restrict__ dq_accum, int T, int H) {
-  __shared__ __attribute__((aligned(16))) bf16_raw k_lds[kKvBlk * kHD];   // 32 KB, swizzled rows
-  __shared__ __attribute__((aligned(16))) bf16_raw q_lds[kQTile * kHD];   // 4 KB
-  __shared__ __attribute__((aligned(16))) bf16_raw do_lds[kQTile * kHD];  // 4 KB
-  __shared__ __attribute__((aligned(16))) bf16_raw ds_lds[kKvBlk * kQTile];  // 16 KB, [key][q]
-  __shared__ __attribute__((aligned(16))) float rowc_lds[2 * kQTile];      // -lse/scale | -delta
+  __shared__ __attribute__((aligned(16))) bf16_raw k_lds[kKvBlk * kHD];          // 32 KB
+  __shared__ __attribute__((aligned(16))) bf16_raw qd_lds[2][2][kQTile * kHD];   // [buf][Q|dO] 32 KB
+  __shared__ __attribute__((aligned(16))) bf16_raw ds_lds[kKvBlk * kQTile];      // [key][q] 32 KB
+  __shared__ __attribute__((aligned(16))) float rowc_lds[2][2 * kQTile];         // -lse/scale | -delta
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int half = lane >> 5, col = lane & 31;
@@ -122,123 +121,152 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
     *reinterpret_cast<ushort8_t*>(&k_lds[tile_chunk_off(r, ch)]) = kz;
   }
 
+  // register staging of one 64-row Q/dO tile (+ its row constants): 2 chunks per thread
+  ushort8_t stg[2];
+  float stc = 0.f;
+  auto load_tile = [&](int q0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int cidx = threadIdx.x + 512 * i;
+      const int which = cidx >> 9, r = (cidx >> 3) & 63, ch = cidx & 7;
+      const int qrow = q0 + r;
+      ushort8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (qrow < T)
+        v = which == 0 ? *reinterpret_cast<const ushort8_t*>(base + (long)qrow * row_stride + ch * 8)
+                       : *reinterpret_cast<const ushort8_t*>(dobase + (long)qrow * out_stride + ch * 8);
+      stg[i] = v;
+    }
+    if (threadIdx.x < 2 * kQTile) {
+      const int qq = q0 + (threadIdx.x & (kQTile - 1));
+      stc = 0.f;
+      if (qq < T) stc = threadIdx.x < kQTile ? -lse_bh[qq] / scale : -delta_bh[qq];
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int cidx = threadIdx.x + 512 * i;
+      const int which = cidx >> 9, r = (cidx >> 3) & 63, ch = cidx & 7;
+      *reinterpret_cast<ushort8_t*>(&qd_lds[buf][which][tile_chunk_off(r, ch)]) = stg[i];
+    }
+    if (threadIdx.x < 2 * kQTile) rowc_lds[buf][threadIdx.x] = stc;
+  };
+
   f32x16 dk[2], dv[2];
   dk[0] = 0.f; dk[1] = 0.f; dv[0] = 0.f; dv[1] = 0.f;
 
-  const int qt_dq = wave & 1;   // dQ output tile of this wave: q rows 16*qt_dq..
-  const int dt_dq = wave >> 1;  //                               d cols 16*dt_dq..
+  const int qt_dq = wave & 3;   // dQ output rows 16*qt_dq .. of the 64-row tile
+  const int dp_dq = wave >> 2;  // dQ output cols 32*dp_dq .. (two 16-wide tiles)
 
-  for (int q0 = kblk0; q0 < T; q0 += kQTile) {
-    // ---- stage Q, dO tiles and the row constants ------------------------------------
-    {
-      const int r = threadIdx.x >> 4, ch = (threadIdx.x >> 1) & 7, which = threadIdx.x & 1;
-      const int qrow = q0 + r;
-      ushort8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (qrow < T) {
-        v = which == 0 ? *reinterpret_cast<const ushort8_t*>(base + (long)qrow * row_stride + ch * 8)
-                       : *reinterpret_cast<const ushort8_t*>(dobase + (long)qrow * out_stride + ch * 8);
-      }
-      *reinterpret_cast<ushort8_t*>((which == 0 ? q_lds : do_lds) + tile_chunk_off(r, ch)) = v;
-      if (threadIdx.x < 2 * kQTile) {
-        const int t = threadIdx.x & (kQTile - 1);
-        const int qq = q0 + t;
-        float val = 0.f;
-        if (qq < T) val = threadIdx.x < kQTile ? -lse_bh[qq] / scale : -delta_bh[qq];
-        rowc_lds[threadIdx.x] = val;
-      }
-    }
-    __syncthreads();
+  load_tile(kblk0);
+  store_tile(0);
+  __syncthreads();
 
-    const bool active = kw0 <= q0 + kQTile - 1 && kw0 < T;  // wave-uniform: any unmasked pair?
-    f32x16 p, ds;
-    if (active) {
-      // row constants as the initial accumulators
+  int it = 0;
+  for (int q0 = kblk0; q0 < T; q0 += kQTile, ++it) {
+    const int cur = it & 1;
+    const bool more = q0 + kQTile < T;
+    if (more) load_tile(q0 + kQTile);  // latency hidden under this tile's MFMAs
+    const bf16_raw* q_lds = qd_lds[cur][0];
+    const bf16_raw* do_lds = qd_lds[cur][1];
+    const float* rowc = rowc_lds[cur];
+
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const f32x4 lc = *reinterpret_cast<const f32x4*>(&rowc_lds[8 * rr + 4 * half]);
-        const f32x4 dc = *reinterpret_cast<const f32x4*>(&rowc_lds[kQTile + 8 * rr + 4 * half]);
+    for (int qs = 0; qs < 2; ++qs) {
+      const int qb0 = q0 + 32 * qs;
+      const bool active = kw0 <= qb0 + 31 && kw0 < T && qb0 < T;  // wave-uniform
+      f32x16 p, ds;
+      if (active) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          p[4 * rr + i] = lc[i];
-          ds[4 * rr + i] = dc[i];
+        for (int rr = 0; rr < 4; ++rr) {
+          const f32x4 lc = *reinterpret_cast<const f32x4*>(&rowc[32 * qs + 8 * rr + 4 * half]);
+          const f32x4 dc = *reinterpret_cast<const f32x4*>(&rowc[kQTile + 32 * qs + 8 * rr + 4 * half]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            p[4 * rr + i] = lc[i];
+            ds[4 * rr + i] = dc[i];
+          }
         }
-      }
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const bf16x8 qa = lds_row_read(q_lds, col, 2 * kk + half);
-        p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[kk], p, 0, 0, 0);
-        const bf16x8 da = lds_row_read(do_lds, col, 2 * kk + half);
-        ds = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[kk], ds, 0, 0, 0);
-      }
-      const bool need_mask = (kw0 + 31 > q0) || (key >= T) || (q0 + kQTile > T);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float pr = exp2f(p[r] * c);
-        if (need_mask) {
-          const int qq = q0 + acc_row(r, half);
-          if (key > qq || key >= T || qq >= T) pr = 0.f;
+        for (int kk = 0; kk < 4; ++kk) {
+          const bf16x8 qa = lds_row_read(q_lds, 32 * qs + col, 2 * kk + half);
+          p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[kk], p, 0, 0, 0);
+          const bf16x8 da = lds_row_read(do_lds, 32 * qs + col, 2 * kk + half);
+          ds = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[kk], ds, 0, 0, 0);
         }
-        p[r] = pr;
-        ds[r] = pr * ds[r];
-      }
-      // dV^T += dO^T P ; dK^T += Q^T dS  (P, dS used in place as B operands)
+        const bool need_mask = (kw0 + 31 > qb0) || (key >= T) || (qb0 + 32 > T);
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const bf16x8 pb = pack_acc8(p, st);
-        const bf16x8 sb = pack_acc8(ds, st);
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const bf16x8 doa = lds_tr_read_operand(do_lds, 16 * st + 4 * half, dt * 32, lane);
-          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(doa, pb, dv[dt], 0, 0, 0);
-          const bf16x8 qa = lds_tr_read_operand(q_lds, 16 * st + 4 * half, dt * 32, lane);
-          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, sb, dk[dt], 0, 0, 0);
+        for (int r = 0; r < 16; ++r) {
+          float pr = exp2f(p[r] * c);
+          if (need_mask) {
+            const int qq = qb0 + acc_row(r, half);
+            if (key > qq || key >= T || qq >= T) pr = 0.f;
+          }
+          p[r] = pr;
+          ds[r] = pr * ds[r];
         }
+        // dV^T += dO^T P ; dK^T += Q^T dS  (P, dS used in place as B operands)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const bf16x8 pb = pack_acc8(p, st);
+          const bf16x8 sb = pack_acc8(ds, st);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            const bf16x8 doa = lds_tr_read_operand(do_lds, 32 * qs + 16 * st + 4 * half, dt * 32, lane);
+            dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(doa, pb, dv[dt], 0, 0, 0);
+            const bf16x8 qa = lds_tr_read_operand(q_lds, 32 * qs + 16 * st + 4 * half, dt * 32, lane);
+            dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, sb, dk[dt], 0, 0, 0);
+          }
+        }
+      } else {
+        ds = 0.f;
       }
-    } else {
-      ds = 0.f;
-    }
-    // dS^T image: [key within block][q], lane writes its key's q rows 8g+4h .. +3 (8 bytes)
-    {
+      // dS^T image [key][q]: this lane's key, q rows 32 qs + 8g + 4h .. +3 (one 8-byte write each)
       const int kl = 32 * wave + col;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         ushort4_t v;
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = f2bf(ds[4 * g + i]);
-        *reinterpret_cast<ushort4_t*>(&ds_lds[kl * kQTile + 8 * g + 4 * half]) = v;
+        *reinterpret_cast<ushort4_t*>(&ds_lds[tile_elem_off(kl, 32 * qs + 8 * g + 4 * half)]) = v;
       }
     }
     __syncthreads();
 
-    // ---- dQ[q0 + 16 qt .., 16 dt ..] += dS K over the block's 256 keys (16x16x32 MFMA) ----
+    // ---- dQ[q0 + 16 qt .., 32 dp + (0..31)] += dS K over the block's 256 keys (16x16x32) ----
     {
       const int i = lane & 15, g = lane >> 4;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      constexpr int nks = kKvBlk / 32;  // keys >= T carry K = 0 and dS = 0
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+      typedef short short8v __attribute__((ext_vector_type(8)));
 #pragma unroll
-      for (int ks = 0; ks < nks; ++ks) {
-        const int key0 = 32 * ks + 8 * g + (i >> 2);
+      for (int ks = 0; ks < kKvBlk / 32; ++ks) {
+        const int krow = 32 * ks + 8 * g + (i >> 2);
         const int qcol = 16 * qt_dq + 4 * (i & 3);
-        const short4v a_lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)&ds_lds[key0 * kQTile + qcol]);
-        const short4v a_hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)&ds_lds[(key0 + 4) * kQTile + qcol]);
-        const int dcol = 16 * dt_dq + 4 * (i & 3);
-        const short4v b_lo = tr_read(k_lds, key0, dcol);
-        const short4v b_hi = tr_read(k_lds, key0 + 4, dcol);
-        typedef short short8v __attribute__((ext_vector_type(8)));
+        const short4v a_lo = tr_read(ds_lds, krow, qcol);
+        const short4v a_hi = tr_read(ds_lds, krow + 4, qcol);
         const short8v av = {a_lo[0], a_lo[1], a_lo[2], a_lo[3], a_hi[0], a_hi[1], a_hi[2], a_hi[3]};
-        const short8v bv = {b_lo[0], b_lo[1], b_lo[2], b_lo[3], b_hi[0], b_hi[1], b_hi[2], b_hi[3]};
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, bv),
-                                                      acc, 0, 0, 0);
+        const int dcol = 32 * dp_dq + 4 * (i & 3);
+        const short4v b0l = tr_read(k_lds, krow, dcol), b0h = tr_read(k_lds, krow + 4, dcol);
+        const short4v b1l = tr_read(k_lds, krow, dcol + 16), b1h = tr_read(k_lds, krow + 4, dcol + 16);
+        const short8v b0 = {b0l[0], b0l[1], b0l[2], b0l[3], b0h[0], b0h[1], b0h[2], b0h[3]};
+        const short8v b1 = {b1l[0], b1l[1], b1l[2], b1l[3], b1h[0], b1h[1], b1h[2], b1h[3]};
+        const bf16x8 a = __builtin_bit_cast(bf16x8, av);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, b0), acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, b1), acc1, 0, 0, 0);
       }
-      const int d = 16 * dt_dq + i;
+      const int d0 = 32 * dp_dq + i;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qq = q0 + 16 * qt_dq + 4 * g + r;
-        if (qq < T) atomicAdd(&dq_accum[(((long)b * T + qq) * H + h) * kHD + d], acc[r] * scale);
+        if (qq < T) {
+          float* dst = &dq_accum[(((long)b * T + qq) * H + h) * kHD + d0];
+          atomicAdd(dst, acc0[r] * scale);
+          atomicAdd(dst + 16, acc1[r] * scale);
+        }
       }
     }
-    // no barrier needed here: the next tile's staging writes only q/do/rowc (not read in the
-    // dQ phase) and its dS writes come after the next barrier
+    if (more) store_tile(cur ^ 1);
+    __syncthreads();
   }
 
   // ---- dK = scale * dK^T, dV = dV^T  -> dqkv[b, key, 1|2, h, :] ------------------------------

@@ -61,6 +61,8 @@ def gemm(M: int = 32768) -> list[dict]:
             ),
         }
         for vname, fn in variants.items():
+            if name == "head" and "llmtrain" in vname:
+                continue  # 3.3 GB dY: beyond the kernel's 32-bit buffer offsets (head uses hipBLASLt)
             ms = timeit(fn)
             rows.append({"gemm": name, "variant": vname, "ms": round(ms, 4), "TFLOPs": round(flops / ms / 1e9, 1)})
             print(json.dumps(rows[-1]), flush=True)

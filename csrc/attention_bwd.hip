@@ -197,7 +197,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
         const bool need_mask = (kw0 + 31 > qb0) || (key >= T) || (qb0 + 32 > T);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float pr = exp2f(p[r] * c);
+          float pr = __builtin_amdgcn_exp2f(p[r] * c);
           if (need_mask) {
             const int qq = qb0 + acc_row(r, half);
             if (key > qq || key >= T || qq >= T) pr = 0.f;

@@ -116,31 +116,31 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
           s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[kk], s[kt], 0, 0, 0);
         }
       }
-      // scale (+ causal / sequence-end mask on diagonal tiles), tile max
+      // causal / sequence-end mask (diagonal tiles only) and the tile max, on RAW scores: the
+      // softmax scale is folded into the exponent below (one FMA per score instead of mul + sub)
       const bool need_mask = (kbase + kKBlk - 1 > q0w) || (kbase + kKBlk > T);
       float tmax = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float t = s[kt][r] * c;
           if (need_mask) {
             const int key = kbase + kt * 32 + acc_row(r, half);
-            if (key > q || key >= T) t = -INFINITY;
+            if (key > q || key >= T) s[kt][r] = -INFINITY;
           }
-          s[kt][r] = t;
-          tmax = fmaxf(tmax, t);
+          tmax = fmaxf(tmax, s[kt][r]);
         }
       }
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float m_new = fmaxf(m_run, tmax);
-      const float alpha = exp2f(m_run - m_new);
+      const float m_new = fmaxf(m_run, tmax);  // raw-score units
+      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
+      const float mc = m_new * c;
       float psum = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(s[kt][r] - m_new);
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], c, -mc));  // v_exp_f32, no denorm fixup
           s[kt][r] = p;
           psum += p;
         }
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
         *reinterpret_cast<ushort4_t*>(dst + dt * 32 + 8 * g + 4 * half) = v;
       }
     }
-    if (half == 0) lse[((long)b * H + h) * T + q] = (m_run + log2f(l_run)) * 0.6931471805599453f;
+    if (half == 0) lse[((long)b * H + h) * T + q] = (m_run * c + log2f(l_run)) * 0.6931471805599453f;
   }
 }
 

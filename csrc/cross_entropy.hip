@@ -82,7 +82,7 @@ __global__ __launch_bounds__(kCeThreads) void ce_fwd_bwd_kernel(
     if (c < nvec) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
-        if (8 * c + i < V) s += exp2f(v[j].get(i) * kLog2e - tmax);
+        if (8 * c + i < V) s += __builtin_amdgcn_exp2f(fmaf(v[j].get(i), kLog2e, -tmax));
     }
   }
   const float ssum = block_sum<kCeWaves>(s, scratch);
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(kCeThreads) void ce_fwd_bwd_kernel(
         const int col = 8 * c + i;
         float gval = 0.f;
         if (col < V) {
-          gval = exp2f(v[j].get(i) * kLog2e - lse2);
+          gval = __builtin_amdgcn_exp2f(fmaf(v[j].get(i), kLog2e, -lse2));
           if (col == label) gval -= 1.f;
           gval *= w;
         }

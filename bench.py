@@ -74,7 +74,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", choices=sorted(MODELS), default="gpt2-124m")
-    ap.add_argument("--micro-batch", type=int, default=32, help="sequences per GPU per micro-step")
+    ap.add_argument("--micro-batch", type=int, default=64, help="sequences per GPU per micro-step")
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--path", choices=["fused", "module"], default="fused")

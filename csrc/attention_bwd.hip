@@ -19,6 +19,9 @@
 //    with 16x16x32 MFMAs over the block's 256 keys, then added to an f32 dQ buffer with
 //    no-return float atomics (dQ bytes / 1.3 TB/s is the floor of this design; a 256-key block
 //    halves it vs 128).  A tiny epilogue kernel converts dQ to bf16 into the packed dqkv.
+#include <cstdlib>
+#include <cstring>
+
 #include "attention_common.h"
 
 namespace llmt {
@@ -68,6 +71,7 @@ __global__ __launch_bounds__(256) void attn_dq_store_kernel(const float* __restr
   *reinterpret_cast<ushort8_t*>(dqkv + (bt * 3 * H + h) * kHD + 8 * c) = pack8(f);
 }
 
+template <bool DQ_ATOMICS>
 __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __restrict__ qkv,
                                                           const bf16_raw* __restrict__ dout,
                                                           const float* __restrict__ lse,
@@ -79,7 +83,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   __shared__ __attribute__((aligned(16))) bf16_raw ds_lds[kKvBlk * kQTile];      // [key][q] 32 KB
   __shared__ __attribute__((aligned(16))) float rowc_lds[2][2 * kQTile];         // -lse/scale | -delta
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably wave-uniform
   const int half = lane >> 5, col = lane & 31;
   const int kb = blockIdx.x;
   const int bh = blockIdx.y;
@@ -194,17 +199,20 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
           const bf16x8 da = lds_row_read(do_lds, 32 * qs + col, 2 * kk + half);
           ds = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[kk], ds, 0, 0, 0);
         }
-        const bool need_mask = (kw0 + 31 > qb0) || (key >= T) || (qb0 + 32 > T);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float pr = __builtin_amdgcn_exp2f(p[r] * c);
-          if (need_mask) {
-            const int qq = qb0 + acc_row(r, half);
-            if (key > qq || key >= T || qq >= T) pr = 0.f;
+        for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(p[r] * c);
+        // causal / sequence-end mask, diagonal and tail tiles only (wave-uniform branch): element
+        // r is query qb0 + 4*half + (r&3) + 8(r>>2), valid iff key <= query < T (branch-free)
+        if ((kw0 + 31 > qb0) || (kw0 + 32 > T) || (qb0 + 32 > T)) {
+          const int lo = key - qb0 - 4 * half, hi = T - 1 - qb0 - 4 * half;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int roff = (r & 3) + 8 * (r >> 2);
+            p[r] = (roff < lo || roff > hi) ? 0.f : p[r];
           }
-          p[r] = pr;
-          ds[r] = pr * ds[r];
         }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ds[r] = p[r] * ds[r];
         // dV^T += dO^T P ; dK^T += Q^T dS  (P, dS used in place as B operands)
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
@@ -260,8 +268,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
         const int qq = q0 + 16 * qt_dq + 4 * g + r;
         if (qq < T) {
           float* dst = &dq_accum[(((long)b * T + qq) * H + h) * kHD + d0];
-          atomicAdd(dst, acc0[r] * scale);
-          atomicAdd(dst + 16, acc1[r] * scale);
+          if (DQ_ATOMICS) {
+            atomicAdd(dst, acc0[r] * scale);
+            atomicAdd(dst + 16, acc1[r] * scale);
+          } else {  // timing experiment only (LLMT_EXPERIMENT=attn_no_dq): wrong dQ
+            asm volatile("" ::"v"(acc0[r]), "v"(acc1[r]));
+          }
         }
       }
     }
@@ -301,7 +313,12 @@ hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, c
   hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, stream,
                      (const bf16_raw*)dout, (const bf16_raw*)out, delta, T, H, rows);
   const int nkb = (T + attn::kKvBlk - 1) / attn::kKvBlk;
-  hipLaunchKernelGGL(attn::attn_bwd_kernel, dim3(nkb, B * H), dim3(512), 0, stream, (const bf16_raw*)qkv,
+  static const bool no_dq = [] {
+    const char* e = getenv("LLMT_EXPERIMENT");
+    return e != nullptr && strcmp(e, "attn_no_dq") == 0;
+  }();
+  auto kern = no_dq ? attn::attn_bwd_kernel<false> : attn::attn_bwd_kernel<true>;
+  hipLaunchKernelGGL(kern, dim3(nkb, B * H), dim3(512), 0, stream, (const bf16_raw*)qkv,
                      (const bf16_raw*)dout, lse, delta, (bf16_raw*)dqkv, dq_accum, T, H);
   const long n8 = rows * attn::kHD / 8;
   hipLaunchKernelGGL(attn::attn_dq_store_kernel, dim3((n8 + 255) / 256), dim3(256), 0, stream, dq_accum,

@@ -35,7 +35,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
                                                           float* __restrict__ lse, int T, int H,
                                                           int nqb) {
   __shared__ __attribute__((aligned(16))) bf16_raw smem[2][2][kKBlk * kHD];  // [buf][K|V][tile]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  // readfirstlane makes the wave index (and every tile/mask decision derived from it) provably
+  // wave-uniform, so hipcc emits scalar branches instead of per-lane exec-mask control flow
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int half = lane >> 5, col = lane & 31;
   const int qb = nqb - 1 - (int)blockIdx.x;  // heavy blocks first
   const int bh = blockIdx.y;
@@ -118,19 +121,21 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
       }
       // causal / sequence-end mask (diagonal tiles only) and the tile max, on RAW scores: the
       // softmax scale is folded into the exponent below (one FMA per score instead of mul + sub)
-      const bool need_mask = (kbase + kKBlk - 1 > q0w) || (kbase + kKBlk > T);
+      const bool need_mask = (kbase + kKBlk - 1 > q0w) || (kbase + kKBlk > T);  // wave-uniform
+      if (need_mask) {
+        // key offset within the tile, (r&3) + 8(r>>2) + 4*half + 32*kt, must be <= lim
+        const int lim = min(q, T - 1) - kbase - 4 * half;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            s[kt][r] = ((r & 3) + 8 * (r >> 2) + 32 * kt > lim) ? -INFINITY : s[kt][r];
+      }
       float tmax = -INFINITY;
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
+      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          if (need_mask) {
-            const int key = kbase + kt * 32 + acc_row(r, half);
-            if (key > q || key >= T) s[kt][r] = -INFINITY;
-          }
-          tmax = fmaxf(tmax, s[kt][r]);
-        }
-      }
+        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, s[kt][r]);
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float m_new = fmaxf(m_run, tmax);  // raw-score units
       const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);

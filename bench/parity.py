@@ -1,0 +1,127 @@
+"""Val-loss parity: the fused MI355X engine against torch-module training of the same model.
+
+    python bench/parity.py --steps 300 --micro-batch 32            # GPT-2 124M, one MI355X
+    python bench/parity.py --model tiny --device cpu --steps 30      # plumbing check on CPU
+
+Every path trains the reference GPT architecture from the SAME seed on the SAME synthetic token
+stream (seeded sparse Markov windows — learnable, so the loss falls well below ln V) with the same
+optimizer/schedule, then reports the full-val-split loss.  Paths:
+
+* ``fused``       — llmtrain engine: hand-written gfx950 kernels, bf16 compute, fp32 master weights;
+* ``module_bf16`` — the torch nn.Module path under bf16 autocast (SDPA attention, torch AdamW);
+* ``module_fp32`` — the torch nn.Module path in fp32: the reference's numerics (gpt.py:35-76,
+                    trainer.py:93-97 AdamW, :390-393 clip) — the parity oracle.
+
+One JSON line per path plus a summary line with the relative val-loss gaps.  The default schedule
+(lr 3e-4, warm-up over the first third, 32 x 1024-token sequences per step) keeps GPT-2 124M out of
+the loss-spike regime: with lr 6e-4 / 16 sequences all three paths spike at the same step (their
+per-step losses agree to ~1e-4 up to there, see ``--trajectory``), after which the chaotic dynamics
+amplify rounding differences into O(1) val-loss differences that say nothing about the kernels.  "Parity" means the
+bf16 paths land within a few 1e-3 relative of the fp32 oracle: bf16 rounding makes bit-equality
+impossible, and two bf16 paths with different kernel orderings differ from each other by the same
+order as each differs from fp32.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+MODELS = {
+    "gpt2-124m": dict(vocab_size=50257, block_size=1024, d_model=768, n_layers=12, n_heads=12, d_ff=3072),
+    "small": dict(vocab_size=50257, block_size=256, d_model=384, n_layers=6, n_heads=6, d_ff=1536),
+    "tiny": dict(vocab_size=512, block_size=64, d_model=64, n_layers=2, n_heads=2, d_ff=128),
+}
+
+
+def run_path(path: str, args: argparse.Namespace) -> dict:
+    from llmtrain.config.schemas import RunConfig
+    from llmtrain.training.trainer import Trainer
+
+    model = dict(MODELS[args.model], name="gpt", dropout=0.0, tie_embeddings=True)
+    fused = path == "fused"
+    model["extra"] = {"fused": fused}
+    precision = "fp32" if path == "module_fp32" else "bf16"
+    if args.device == "cpu":
+        precision = "fp32"
+    cfg = RunConfig.model_validate({
+        "schema_version": 1,
+        "run": {"name": f"parity-{path}", "seed": args.seed, "device": args.device, "precision": precision},
+        "model": model,
+        "data": {"name": "synthetic_tokens", "num_workers": 0,
+                 "extra": {"train_sequences": args.steps * args.micro_batch, "val_sequences": args.val_sequences,
+                           "branching": args.branching}},
+        "trainer": {"max_steps": args.steps, "micro_batch_size": args.micro_batch, "grad_accum_steps": 1,
+                    "lr": args.lr, "weight_decay": 0.1, "warmup_steps": args.warmup if args.warmup is not None else max(1, args.steps // 3),
+                    "max_grad_norm": 1.0, "log_every_steps": max(1, args.steps // 5),
+                    "eval_every_steps": args.steps, "save_every_steps": 10**9},
+        "ddp": {"enabled": False}, "mlflow": {"enabled": False},
+        "logging": {"log_to_file": False}, "output": {"root_dir": "/tmp/llmtrain_parity_runs"},
+    })
+    t0 = time.perf_counter()
+    trainer = Trainer(cfg)
+    if args.trajectory:
+        batches = trainer.batch_stream()
+        losses, norms = [], []
+        for _ in range(args.trajectory):
+            loss, _ = trainer.train_step(batches)
+            losses.append(round(float(loss), 4))
+            norms.append(round(float(trainer.last_grad_norm), 4))
+        return {"path": path, "losses": losses, "grad_norms": norms}
+    result = trainer.fit()
+    return {
+        "path": path,
+        "fused_engine": bool(getattr(trainer, "_policy").use_fused),
+        "precision": precision,
+        "first_step_loss": result.first_step_loss,
+        "final_train_loss": round(result.final_loss, 5),
+        "val_loss": None if result.final_val_loss is None else round(result.final_val_loss, 5),
+        "wall_s": round(time.perf_counter() - t0, 1),
+    }
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--model", choices=sorted(MODELS), default="gpt2-124m")
+    ap.add_argument("--device", default="cuda")
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--micro-batch", type=int, default=32)
+    ap.add_argument("--val-sequences", type=int, default=64)
+    ap.add_argument("--branching", type=int, default=4)
+    ap.add_argument("--lr", type=float, default=3e-4)
+    ap.add_argument("--warmup", type=int, default=None, help="LR warm-up steps (default: steps // 3)")
+    ap.add_argument("--seed", type=int, default=1337)
+    ap.add_argument("--paths", default="fused,module_bf16,module_fp32")
+    ap.add_argument("--trajectory", type=int, default=0, help="print per-step losses/grad norms of N steps instead")
+    args = ap.parse_args()
+
+    rows = []
+    for path in args.paths.split(","):
+        if path == "fused" and args.device == "cpu":
+            continue  # the fused engine is the GPU path; its CPU reference ops are covered by tests
+        rows.append(run_path(path, args))
+        print(json.dumps(rows[-1]), flush=True)
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+    if args.trajectory:
+        return 0
+    oracle = next((r for r in rows if r["path"] == "module_fp32"), None)
+    summary: dict = {"model": args.model, "steps": args.steps, "micro_batch": args.micro_batch,
+                     "tokens": args.steps * args.micro_batch * MODELS[args.model]["block_size"]}
+    if oracle and oracle["val_loss"]:
+        for r in rows:
+            if r is not oracle and r["val_loss"] is not None:
+                summary[f"rel_gap_{r['path']}_vs_fp32"] = round((r["val_loss"] - oracle["val_loss"]) / oracle["val_loss"], 5)
+    print(json.dumps({"parity_summary": summary}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

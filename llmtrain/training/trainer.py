@@ -159,6 +159,7 @@ class Trainer:
             keep = int(cfg.trainer.extra.get("keep_last_k", 3))
             self._ckpt_mgr = CheckpointManager(run_dir / "checkpoints", keep_last_k=keep)
         self._run_dir = run_dir
+        self.last_grad_norm: torch.Tensor | None = None
         logger.info(
             "trainer: device=%s compute_dtype=%s fused=%s ddp=%s",
             self._device, self._policy.compute_dtype, self._policy.use_fused, self._is_ddp_active,
@@ -310,11 +311,12 @@ class Trainer:
             finish()
         max_norm = self._cfg.trainer.max_grad_norm
         if isinstance(self._optimizer, FusedAdamW):
-            _, coef = fused_clip_coef(self._optimizer.store, max_norm)
+            norm, coef = fused_clip_coef(self._optimizer.store, max_norm)
             self._optimizer.step(grad_scale=coef)
         else:
-            torch.nn.utils.clip_grad_norm_(self._model.parameters(), max_norm)
+            norm = torch.nn.utils.clip_grad_norm_(self._model.parameters(), max_norm)
             self._optimizer.step()
+        self.last_grad_norm = norm  # pre-clip global L2 norm, device scalar (no host sync)
         self._scheduler.step()
 
     def batch_stream(self) -> _Batches:

@@ -31,7 +31,7 @@ def timeit(fn, iters: int = 20, warmup: int = 5) -> float:
     return times[len(times) // 2]  # median ms
 
 
-def gemm(M: int = 32768) -> list[dict]:
+def gemm(M: int = 32768, only: str = "") -> list[dict]:
     from llmtrain.ops import _ext
 
     _ext.require()
@@ -52,7 +52,9 @@ def gemm(M: int = 32768) -> list[dict]:
             "dW mm bf16": lambda: torch.mm(dy.t(), x),
             "dW mm bf16 + add": lambda: acc.add_(torch.mm(dy.t(), x)),
             "dW^T mm bf16 (x^T dy)": lambda: torch.mm(x.t(), dy),
-            "dW llmtrain split-K wgrad": lambda: torch.ops.llmtrain_hip.wgrad_gemm(dy, x, acc, 0),
+            "dW llmtrain wgrad auto": lambda: torch.ops.llmtrain_hip.wgrad_gemm(dy, x, acc, 0, 0),
+            "dW llmtrain wgrad tile128": lambda: torch.ops.llmtrain_hip.wgrad_gemm(dy, x, acc, 0, 128),
+            "dW llmtrain wgrad tile256": lambda: torch.ops.llmtrain_hip.wgrad_gemm(dy, x, acc, 0, 256),
             "dW hipblaslt bmm split8 + sum": lambda: acc.add_(
                 torch.bmm(dy.view(8, M // 8, N).transpose(1, 2), x.view(8, M // 8, K)).float().sum(0)
             ),
@@ -61,6 +63,8 @@ def gemm(M: int = 32768) -> list[dict]:
             ),
         }
         for vname, fn in variants.items():
+            if only == "wgrad" and not ("llmtrain" in vname or "addmm" in vname):
+                continue
             if name == "head" and "llmtrain" in vname:
                 continue  # 3.3 GB dY: beyond the kernel's 32-bit buffer offsets (head uses hipBLASLt)
             ms = timeit(fn)
@@ -103,6 +107,8 @@ def attn(B: int = 32, T: int = 1024, H: int = 12) -> list[dict]:
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("gemm", "all"):
-        gemm()
+        gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 32768)
+    if what == "wgrad":  # just the weight-gradient variants
+        gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 65536, only="wgrad")
     if what in ("attn", "all"):
         attn()

@@ -289,7 +289,7 @@ Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const 
 }
 
 // ---- weight-gradient GEMM --------------------------------------------------------------------
-void wgrad_gemm(const Tensor& dy, const Tensor& x, Tensor c, int64_t split) {
+void wgrad_gemm(const Tensor& dy, const Tensor& x, Tensor c, int64_t split, int64_t tile) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && c.is_cuda(), "wgrad_gemm: GPU tensors required");
   check_dtype(dy, at::kBFloat16, "dy");
   check_dtype(x, at::kBFloat16, "x");
@@ -301,7 +301,7 @@ void wgrad_gemm(const Tensor& dy, const Tensor& x, Tensor c, int64_t split) {
   at::hip::HIPGuardMasqueradingAsCUDA guard(c.device());
   check_hip(llmt::launch_wgrad_gemm(dy.data_ptr(), (int)dy.stride(0), x.data_ptr(), (int)x.stride(0),
                                     c.data_ptr<float>(), (int)c.stride(0), (int)M, (int)N, (int)K, (int)split,
-                                    cur_stream()),
+                                    (int)tile, cur_stream()),
             "wgrad_gemm");
 }
 
@@ -371,7 +371,7 @@ TORCH_LIBRARY(llmtrain_hip, m) {
   m.def("embedding_bwd(Tensor dx, Tensor ids, Tensor(a!) dwte, Tensor(b!) dwpe) -> ()");
   m.def("attn_fwd(Tensor qkv, int B, int T, int H) -> (Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, int B, int T, int H) -> Tensor");
-  m.def("wgrad_gemm(Tensor dy, Tensor x, Tensor(a!) c, int split=0) -> ()");
+  m.def("wgrad_gemm(Tensor dy, Tensor x, Tensor(a!) c, int split=0, int tile=0) -> ()");
   m.def("sumsq(Tensor x) -> Tensor");
   m.def("adamw_flat(Tensor(a!) param, Tensor grad, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor(d!)? shadow,"
         " float lr, float beta1, float beta2, float eps, float weight_decay, int step, Tensor? grad_scale) -> ()");

@@ -87,9 +87,9 @@ hipError_t launch_sumsq(const float* x, long long n, float* partials, float* out
                         hipStream_t stream);
 
 // ---- weight-gradient GEMM: C[N, K] (f32) += dY[M, N]^T X[M, K] (bf16), split-K + atomics --
-// split <= 0 picks a split that yields ~2 workgroups per CU.
+// split <= 0 / tile == 0 let the launcher's cost model choose (tile 128 or 256 forces one).
 hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N,
-                             int K, int split, hipStream_t stream);
+                             int K, int split, int tile, hipStream_t stream);
 
 // ---- causal flash attention (head_dim 64) ----------------------------------------------
 // qkv [B, T, 3, H, 64] bf16 (the packed projection output), out [B, T, H, 64] bf16,

@@ -122,7 +122,7 @@ def wgrad_accum(dst, dy, x) -> None:
     """``dst (fp32 [N, K]) += dy[M, N]^T @ x[M, K]`` — split-K MFMA GEMM with atomic fp32
     accumulation on GPU (``dy`` may be a column slice with a larger row stride)."""
     if _on_gpu(dst):
-        hip_ops().wgrad_gemm(dy, x, dst, 0)
+        hip_ops().wgrad_gemm(dy, x, dst, 0, 0)
     else:
         dst.addmm_(dy.t().float(), x.float())
 

@@ -193,21 +193,23 @@ def test_attention_causality(gpu_device):
     assert torch.equal(out1[:200], out2[:200])
 
 
+@pytest.mark.parametrize("tile", [0, 128, 256])
 @pytest.mark.parametrize("M,N,K,lda", [(4096, 768, 768, 768), (2048, 2304, 768, 2304), (1000, 200, 72, 200),
-                                        (3000, 1000, 768, 1024)])
-def test_wgrad_gemm(gpu_device, M, N, K, lda):
-    """Split-K MFMA weight-gradient GEMM accumulates dY^T X into an existing fp32 buffer; also
-    with a column-slice dY (row stride lda > N, like the vocab-padded logits)."""
+                                        (3000, 1000, 768, 1024), (2080, 1600, 4800, 1600)])
+def test_wgrad_gemm(gpu_device, M, N, K, lda, tile):
+    """Split-K MFMA weight-gradient GEMM accumulates dY^T X into an existing fp32 buffer, for both
+    tile configurations and the cost-model choice; also with a column-slice dY (row stride
+    lda > N, like the vocab-padded logits) and GPT-2 XL widths that are not tile multiples."""
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
     dy_full = torch.randn(M, lda, generator=g).to(gpu_device, torch.bfloat16)
     dy = dy_full[:, :N]
     x = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)
     c = torch.randn(N, K, generator=g).to(gpu_device)
     want = c + dy.float().t() @ x.float()
-    hip().wgrad_gemm(dy, x, c, 0)
+    hip().wgrad_gemm(dy, x, c, 0, tile)
     scale = want.abs().max().item()
     _close(c, want, 1e-3 * scale, 1e-3, "wgrad")
     # an explicit split also works and is additive
     c2 = torch.zeros(N, K, device=gpu_device)
-    hip().wgrad_gemm(dy, x, c2, 3)
+    hip().wgrad_gemm(dy, x, c2, 3, tile)
     _close(c2, dy.float().t() @ x.float(), 1e-3 * scale, 1e-3, "wgrad split=3")

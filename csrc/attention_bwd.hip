@@ -71,23 +71,37 @@ __global__ __launch_bounds__(256) void attn_dq_store_kernel(const float* __restr
   *reinterpret_cast<ushort8_t*>(dqkv + (bt * 3 * H + h) * kHD + 8 * c) = pack8(f);
 }
 
+// raw 16-byte / 4-byte buffer loads: offsets past the descriptor's record count read as zero
+__device__ __forceinline__ ushort8_t buf_load16(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
+  return __builtin_bit_cast(ushort8_t, v);
+}
+__device__ __forceinline__ float buf_load_f32(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
+
+// K^T image [64 d][256 keys]: 512-byte rows, 16-byte chunk index XOR-swizzled by (d & 15) so the
+// 16 rows a ds_read_b128 lane group touches land on 16 distinct chunks (all 64 banks)
+__device__ __forceinline__ int kt_off(int d, int key) { return d * kKvBlk + ((((key >> 3) ^ (d & 15))) << 3) + (key & 7); }
+
 template <bool DQ_ATOMICS>
 __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __restrict__ qkv,
                                                           const bf16_raw* __restrict__ dout,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta,
                                                           bf16_raw* __restrict__ dqkv,
-                                                          float* __restrict__ dq_accum, int T, int H) {
-  __shared__ __attribute__((aligned(16))) bf16_raw k_lds[kKvBlk * kHD];          // 32 KB
-  __shared__ __attribute__((aligned(16))) bf16_raw qd_lds[2][2][kQTile * kHD];   // [buf][Q|dO] 32 KB
-  __shared__ __attribute__((aligned(16))) bf16_raw ds_lds[kKvBlk * kQTile];      // [key][q] 32 KB
-  __shared__ __attribute__((aligned(16))) float rowc_lds[2][2 * kQTile];         // -lse/scale | -delta
+                                                          float* __restrict__ dq_accum, int T, int H, int nkb) {
+  __shared__ __attribute__((aligned(16))) bf16_raw kt_lds[kHD * kKvBlk];             // K^T, 32 KB
+  __shared__ __attribute__((aligned(16))) bf16_raw qd_lds[2][2][kQTile * kHD];      // [buf][Q|dO] 32 KB
+  __shared__ __attribute__((aligned(16))) bf16_raw ds_lds[2][kKvBlk * kQTile];      // [buf][key][q] 64 KB
+  __shared__ __attribute__((aligned(16))) float rowc_lds[2][2 * kQTile];            // lse*log2e | delta
 
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably wave-uniform
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int half = lane >> 5, col = lane & 31;
-  const int kb = blockIdx.x;
-  const int bh = blockIdx.y;
+  const int bh = blockIdx.x;                 // all key blocks of one (b, h) share an XCD
+  const int kb = nkb - 1 - (int)blockIdx.y;  // ... and the heaviest (first) key blocks go first
   const int b = bh / H, h = bh - b * H;
   const long row_stride = 3L * H * kHD;
   const bf16_raw* base = qkv + (long)b * T * row_stride + (long)h * kHD;
@@ -95,6 +109,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   const long out_stride = (long)H * kHD;
   const float* lse_bh = lse + ((long)b * H + h) * T;
   const float* delta_bh = delta + ((long)b * H + h) * T;
+  // descriptors bounded at row T of this (b, h): rows past the sequence load as zeros
+  const __amdgpu_buffer_rsrc_t r_q = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0,
+                                                                        (int)((T - 1) * row_stride + kHD) * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r_do = __builtin_amdgcn_make_buffer_rsrc((void*)dobase, (short)0,
+                                                                         (int)((T - 1) * out_stride + kHD) * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r_lse = __builtin_amdgcn_make_buffer_rsrc((void*)lse_bh, (short)0, T * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r_del = __builtin_amdgcn_make_buffer_rsrc((void*)delta_bh, (short)0, T * 4, 0x00020000);
 
   const int kblk0 = kb * kKvBlk;
   const int kw0 = kblk0 + 32 * wave;  // first key of this wave
@@ -107,23 +128,16 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   bf16x8 kf[4], vf[4];
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
-    ushort8_t kz = {0, 0, 0, 0, 0, 0, 0, 0}, vz = kz;
-    if (key < T) {
-      const bf16_raw* src = base + (long)key * row_stride + 16 * kk + 8 * half;
-      kz = *reinterpret_cast<const ushort8_t*>(src + kHD * H);
-      vz = *reinterpret_cast<const ushort8_t*>(src + 2 * kHD * H);
-    }
-    kf[kk] = __builtin_bit_cast(bf16x8, kz);
-    vf[kk] = __builtin_bit_cast(bf16x8, vz);
+    const int off = (int)(key * row_stride + 16 * kk + 8 * half) * 2;
+    kf[kk] = __builtin_bit_cast(bf16x8, buf_load16(r_q, off + kHD * H * 2));
+    vf[kk] = __builtin_bit_cast(bf16x8, buf_load16(r_q, off + 2 * kHD * H * 2));
   }
-  // whole 256-key K block into LDS (B operand of dQ = dS K through transposed reads)
+  // K^T image for dQ = dS K (B operand read 8 keys at a time); written from the K fragments
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int cidx = threadIdx.x + 512 * i;
-    const int r = cidx >> 3, ch = cidx & 7;
-    ushort8_t kz = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (kblk0 + r < T) kz = *reinterpret_cast<const ushort8_t*>(base + (long)(kblk0 + r) * row_stride + kHD * H + ch * 8);
-    *reinterpret_cast<ushort8_t*>(&k_lds[tile_chunk_off(r, ch)]) = kz;
+  for (int kk = 0; kk < 4; ++kk) {
+    const ushort8_t kv = __builtin_bit_cast(ushort8_t, kf[kk]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) kt_lds[kt_off(16 * kk + 8 * half + j, 32 * wave + col)] = kv[j];
   }
 
   // register staging of one 64-row Q/dO tile (+ its row constants): 2 chunks per thread
@@ -133,28 +147,24 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int cidx = threadIdx.x + 512 * i;
-      const int which = cidx >> 9, r = (cidx >> 3) & 63, ch = cidx & 7;
+      const int r = (cidx >> 3) & 63, ch = cidx & 7;
       const int qrow = q0 + r;
-      ushort8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (qrow < T)
-        v = which == 0 ? *reinterpret_cast<const ushort8_t*>(base + (long)qrow * row_stride + ch * 8)
-                       : *reinterpret_cast<const ushort8_t*>(dobase + (long)qrow * out_stride + ch * 8);
-      stg[i] = v;
+      stg[i] = i == 0 ? buf_load16(r_q, (int)(qrow * row_stride + ch * 8) * 2)
+                      : buf_load16(r_do, (int)(qrow * out_stride + ch * 8) * 2);
     }
     if (threadIdx.x < 2 * kQTile) {
       const int qq = q0 + (threadIdx.x & (kQTile - 1));
-      stc = 0.f;
-      if (qq < T) stc = threadIdx.x < kQTile ? -lse_bh[qq] / scale : -delta_bh[qq];
+      stc = threadIdx.x < kQTile ? buf_load_f32(r_lse, qq * 4) : buf_load_f32(r_del, qq * 4);
     }
   };
   auto store_tile = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int cidx = threadIdx.x + 512 * i;
-      const int which = cidx >> 9, r = (cidx >> 3) & 63, ch = cidx & 7;
-      *reinterpret_cast<ushort8_t*>(&qd_lds[buf][which][tile_chunk_off(r, ch)]) = stg[i];
+      const int r = (cidx >> 3) & 63, ch = cidx & 7;
+      *reinterpret_cast<ushort8_t*>(&qd_lds[buf][i][tile_chunk_off(r, ch)]) = stg[i];
     }
-    if (threadIdx.x < 2 * kQTile) rowc_lds[buf][threadIdx.x] = stc;
+    if (threadIdx.x < 2 * kQTile) rowc_lds[buf][threadIdx.x] = threadIdx.x < kQTile ? stc * 1.4426950408889634f : stc;
   };
 
   f32x16 dk[2], dv[2];
@@ -163,47 +173,42 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   const int qt_dq = wave & 3;   // dQ output rows 16*qt_dq .. of the 64-row tile
   const int dp_dq = wave >> 2;  // dQ output cols 32*dp_dq .. (two 16-wide tiles)
 
-  load_tile(kblk0);
-  store_tile(0);
-  __syncthreads();
-
-  int it = 0;
-  for (int q0 = kblk0; q0 < T; q0 += kQTile, ++it) {
-    const int cur = it & 1;
-    const bool more = q0 + kQTile < T;
-    if (more) load_tile(q0 + kQTile);  // latency hidden under this tile's MFMAs
-    const bf16_raw* q_lds = qd_lds[cur][0];
-    const bf16_raw* do_lds = qd_lds[cur][1];
-    const float* rowc = rowc_lds[cur];
-
+  // ---- phase A of one 32-row query sub-tile: S, P, dP, dS, dV^T, dK^T, dS^T image ----------
+  // full: the whole 64-row tile lies below the diagonal of every key of the block and inside the
+  // sequence — no activity test, no mask (one body: two specialisations would each hoist their own
+  // loop invariants and overflow the 256-VGPR budget).
+  auto phase_a = [&](bool full, int q0, const bf16_raw* q_lds, const bf16_raw* do_lds, const float* rowc,
+                     bf16_raw* dsimg) {
 #pragma unroll
     for (int qs = 0; qs < 2; ++qs) {
       const int qb0 = q0 + 32 * qs;
-      const bool active = kw0 <= qb0 + 31 && kw0 < T && qb0 < T;  // wave-uniform
-      f32x16 p, ds;
+      const bool active = full || (kw0 <= qb0 + 31 && kw0 < T && qb0 < T);  // wave-uniform
+      f32x16 ds;
       if (active) {
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const f32x4 lc = *reinterpret_cast<const f32x4*>(&rowc[32 * qs + 8 * rr + 4 * half]);
-          const f32x4 dc = *reinterpret_cast<const f32x4*>(&rowc[kQTile + 32 * qs + 8 * rr + 4 * half]);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            p[4 * rr + i] = lc[i];
-            ds[4 * rr + i] = dc[i];
-          }
-        }
+        f32x16 p, dp;
+        p = 0.f;
+        dp = 0.f;
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
           const bf16x8 qa = lds_row_read(q_lds, 32 * qs + col, 2 * kk + half);
           p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[kk], p, 0, 0, 0);
           const bf16x8 da = lds_row_read(do_lds, 32 * qs + col, 2 * kk + half);
-          ds = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[kk], ds, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[kk], dp, 0, 0, 0);
         }
+        __builtin_amdgcn_sched_barrier(0);  // row constants are read after the chains (VGPR budget)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(p[r] * c);
-        // causal / sequence-end mask, diagonal and tail tiles only (wave-uniform branch): element
-        // r is query qb0 + 4*half + (r&3) + 8(r>>2), valid iff key <= query < T (branch-free)
-        if ((kw0 + 31 > qb0) || (kw0 + 32 > T) || (qb0 + 32 > T)) {
+        for (int rr = 0; rr < 4; ++rr) {
+          const f32x4 l2 = *reinterpret_cast<const f32x4*>(&rowc[32 * qs + 8 * rr + 4 * half]);
+          const f32x4 dd = *reinterpret_cast<const f32x4*>(&rowc[kQTile + 32 * qs + 8 * rr + 4 * half]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            p[4 * rr + i] = __builtin_amdgcn_exp2f(fmaf(p[4 * rr + i], c, -l2[i]));
+            dp[4 * rr + i] -= dd[i];
+          }
+        }
+        if (!full && ((kw0 + 31 > qb0) || (kw0 + 32 > T) || (qb0 + 32 > T))) {
+          // causal / sequence-end mask: element r is query qb0 + 4*half + (r&3) + 8(r>>2),
+          // valid iff key <= query < T (branch-free selects)
           const int lo = key - qb0 - 4 * half, hi = T - 1 - qb0 - 4 * half;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -212,7 +217,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
           }
         }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) ds[r] = p[r] * ds[r];
+        for (int r = 0; r < 16; ++r) ds[r] = p[r] * dp[r];
         // dV^T += dO^T P ; dK^T += Q^T dS  (P, dS used in place as B operands)
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
@@ -236,10 +241,31 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
         ushort4_t v;
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = f2bf(ds[4 * g + i]);
-        *reinterpret_cast<ushort4_t*>(&ds_lds[tile_elem_off(kl, 32 * qs + 8 * g + 4 * half)]) = v;
+        *reinterpret_cast<ushort4_t*>(&dsimg[tile_elem_off(kl, 32 * qs + 8 * g + 4 * half)]) = v;
       }
+      // keep the two sub-tiles' live ranges apart: overlapping them exceeds the 256-VGPR budget
+      // of two waves per SIMD (spills)
+      __builtin_amdgcn_sched_barrier(0);
     }
-    __syncthreads();
+  };
+
+  load_tile(kblk0);
+  store_tile(0);
+  __syncthreads();
+
+  int it = 0;
+  for (int q0 = kblk0; q0 < T; q0 += kQTile, ++it) {
+    const int cur = it & 1;
+    const bool more = q0 + kQTile < T;
+    if (more) load_tile(q0 + kQTile);  // latency hidden under this tile's MFMAs
+    const bf16_raw* q_lds = qd_lds[cur][0];
+    const bf16_raw* do_lds = qd_lds[cur][1];
+    bf16_raw* dsimg = ds_lds[cur];
+    phase_a(q0 >= kblk0 + kKvBlk && q0 + kQTile <= T, q0, q_lds, do_lds, rowc_lds[cur], dsimg);
+    if (more) store_tile(cur ^ 1);
+    // one barrier per tile: the dS image and the next Q/dO tile are double-buffered, so the only
+    // hand-off is "phase A of this tile (and the next tile's staging) done by every wave"
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
     // ---- dQ[q0 + 16 qt .., 32 dp + (0..31)] += dS K over the block's 256 keys (16x16x32) ----
     {
@@ -250,17 +276,15 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
       for (int ks = 0; ks < kKvBlk / 32; ++ks) {
         const int krow = 32 * ks + 8 * g + (i >> 2);
         const int qcol = 16 * qt_dq + 4 * (i & 3);
-        const short4v a_lo = tr_read(ds_lds, krow, qcol);
-        const short4v a_hi = tr_read(ds_lds, krow + 4, qcol);
+        const short4v a_lo = tr_read(dsimg, krow, qcol);
+        const short4v a_hi = tr_read(dsimg, krow + 4, qcol);
         const short8v av = {a_lo[0], a_lo[1], a_lo[2], a_lo[3], a_hi[0], a_hi[1], a_hi[2], a_hi[3]};
-        const int dcol = 32 * dp_dq + 4 * (i & 3);
-        const short4v b0l = tr_read(k_lds, krow, dcol), b0h = tr_read(k_lds, krow + 4, dcol);
-        const short4v b1l = tr_read(k_lds, krow, dcol + 16), b1h = tr_read(k_lds, krow + 4, dcol + 16);
-        const short8v b0 = {b0l[0], b0l[1], b0l[2], b0l[3], b0h[0], b0h[1], b0h[2], b0h[3]};
-        const short8v b1 = {b1l[0], b1l[1], b1l[2], b1l[3], b1h[0], b1h[1], b1h[2], b1h[3]};
+        const int kc = 32 * ks + 8 * g;  // first of this lane's 8 keys
+        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(&kt_lds[kt_off(32 * dp_dq + i, kc)]);
+        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(&kt_lds[kt_off(32 * dp_dq + 16 + i, kc)]);
         const bf16x8 a = __builtin_bit_cast(bf16x8, av);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, b0), acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, b1), acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b1, acc1, 0, 0, 0);
       }
       const int d0 = 32 * dp_dq + i;
 #pragma unroll
@@ -277,8 +301,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
         }
       }
     }
-    if (more) store_tile(cur ^ 1);
-    __syncthreads();
   }
 
   // ---- dK = scale * dK^T, dV = dV^T  -> dqkv[b, key, 1|2, h, :] ------------------------------
@@ -318,8 +340,8 @@ hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, c
     return e != nullptr && strcmp(e, "attn_no_dq") == 0;
   }();
   auto kern = no_dq ? attn::attn_bwd_kernel<false> : attn::attn_bwd_kernel<true>;
-  hipLaunchKernelGGL(kern, dim3(nkb, B * H), dim3(512), 0, stream, (const bf16_raw*)qkv,
-                     (const bf16_raw*)dout, lse, delta, (bf16_raw*)dqkv, dq_accum, T, H);
+  hipLaunchKernelGGL(kern, dim3(B * H, nkb), dim3(512), 0, stream, (const bf16_raw*)qkv,
+                     (const bf16_raw*)dout, lse, delta, (bf16_raw*)dqkv, dq_accum, T, H, nkb);
   const long n8 = rows * attn::kHD / 8;
   hipLaunchKernelGGL(attn::attn_dq_store_kernel, dim3((n8 + 255) / 256), dim3(256), 0, stream, dq_accum,
                      (bf16_raw*)dqkv, H, n8);

@@ -16,11 +16,13 @@
 //    as the next MFMA's operand); dO^T and Q^T fragments come from ds_read_b64_tr_b16 on the
 //    same LDS images that serve the row reads (one swizzle, conflict free both ways);
 //  * dS crosses LDS once (as a [key][q] image written 8 bytes per lane) and dQ = dS K is formed
-//    with 16x16x32 MFMAs over the block's 256 keys, then added to an f32 dQ buffer with
-//    no-return float atomics (dQ bytes / 1.3 TB/s is the floor of this design; a 256-key block
-//    halves it vs 128).  A tiny epilogue kernel converts dQ to bf16 into the packed dqkv.
-#include <cstdlib>
-#include <cstring>
+//    with 16x16x32 MFMAs over the block's 256 keys (K^T LDS image, one ds_read_b128 per B
+//    operand); each key block stores its dQ contribution to its OWN fp32 partial plane with
+//    plain stores (4-5x the chip-wide float-atomic rate, and no memset), and a reduce pass sums
+//    the <= T/256 planes per row straight into the packed bf16 dqkv;
+//  * branch-free buffer loads (rows past T read as zero), double-buffered Q/dO and dS images,
+//    one barrier per query tile; heaviest key blocks dispatched first, the key blocks of one
+//    (batch, head) on one XCD (shared Q/dO in its L2).
 
 #include "attention_common.h"
 
@@ -56,19 +58,32 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
   }
 }
 
-// dqkv[b, t, 0, h, :] = bf16(dq_accum[b, t, h, :])
-__global__ __launch_bounds__(256) void attn_dq_store_kernel(const float* __restrict__ dq, bf16_raw* __restrict__ dqkv,
-                                                            int H, long n8) {
+// dqkv[b, t, 0, h, :] = bf16(sum over key blocks kb <= t / 256 of dq_part[kb][b, h, t, :]):
+// the main kernel stores each key block's dQ contribution with plain stores (no memset, no
+// atomics); rows only ever read the partials their causal key blocks wrote.
+__global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const float* __restrict__ part, bf16_raw* __restrict__ dqkv,
+                                                             int T, int H, int nkb, long n8) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // one 8-element chunk
   if (i >= n8) return;
-  const long row = i >> 3;  // (b*T + t)*H + h
+  const long row = i >> 3;  // (b*H + h)*T + t
   const int c = (int)(i & 7);
-  const long bt = row / H;
-  const int h = (int)(row - bt * H);
-  const float4_t* src = reinterpret_cast<const float4_t*>(dq + row * kHD + 8 * c);
-  const float4_t a = src[0], b2 = src[1];
-  const float f[8] = {a[0], a[1], a[2], a[3], b2[0], b2[1], b2[2], b2[3]};
-  *reinterpret_cast<ushort8_t*>(dqkv + (bt * 3 * H + h) * kHD + 8 * c) = pack8(f);
+  const long bh = row / T;
+  const int t = (int)(row - bh * T);
+  const long b = bh / H;
+  const int h = (int)(bh - b * H);
+  const long plane = n8 * 8;  // floats per key-block partial
+  const int last = min(t / kKvBlk, nkb - 1);
+  float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int kb = 0; kb <= last; ++kb) {
+    const float4_t* src = reinterpret_cast<const float4_t*>(part + kb * plane + row * kHD + 8 * c);
+    const float4_t x = src[0], y = src[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f[j] += x[j];
+      f[4 + j] += y[j];
+    }
+  }
+  *reinterpret_cast<ushort8_t*>(dqkv + ((b * T + t) * 3L * H + h) * kHD + 8 * c) = pack8(f);
 }
 
 // raw 16-byte / 4-byte buffer loads: offsets past the descriptor's record count read as zero
@@ -85,13 +100,12 @@ __device__ __forceinline__ float buf_load_f32(__amdgpu_buffer_rsrc_t r, int byte
 // 16 rows a ds_read_b128 lane group touches land on 16 distinct chunks (all 64 banks)
 __device__ __forceinline__ int kt_off(int d, int key) { return d * kKvBlk + ((((key >> 3) ^ (d & 15))) << 3) + (key & 7); }
 
-template <bool DQ_ATOMICS>
 __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __restrict__ qkv,
                                                           const bf16_raw* __restrict__ dout,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta,
                                                           bf16_raw* __restrict__ dqkv,
-                                                          float* __restrict__ dq_accum, int T, int H, int nkb) {
+                                                          float* __restrict__ dq_part, int T, int H, int nkb) {
   __shared__ __attribute__((aligned(16))) bf16_raw kt_lds[kHD * kKvBlk];             // K^T, 32 KB
   __shared__ __attribute__((aligned(16))) bf16_raw qd_lds[2][2][kQTile * kHD];      // [buf][Q|dO] 32 KB
   __shared__ __attribute__((aligned(16))) bf16_raw ds_lds[2][kKvBlk * kQTile];      // [buf][key][q] 64 KB
@@ -286,18 +300,17 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
         acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b0, acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b1, acc1, 0, 0, 0);
       }
+      // this key block's dQ contribution -> its own fp32 partial plane (plain stores, 64-byte
+      // row segments per 16 lanes); attn_dq_reduce_kernel sums the planes
       const int d0 = 32 * dp_dq + i;
+      float* plane = dq_part + ((long)kb * gridDim.x + bh) * T * kHD;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qq = q0 + 16 * qt_dq + 4 * g + r;
         if (qq < T) {
-          float* dst = &dq_accum[(((long)b * T + qq) * H + h) * kHD + d0];
-          if (DQ_ATOMICS) {
-            atomicAdd(dst, acc0[r] * scale);
-            atomicAdd(dst + 16, acc1[r] * scale);
-          } else {  // timing experiment only (LLMT_EXPERIMENT=attn_no_dq): wrong dQ
-            asm volatile("" ::"v"(acc0[r]), "v"(acc1[r]));
-          }
+          float* dst = plane + (long)qq * kHD + d0;
+          dst[0] = acc0[r] * scale;
+          dst[16] = acc1[r] * scale;
         }
       }
     }
@@ -326,25 +339,23 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
 
 }  // namespace attn
 
+long attn_bwd_workspace_floats(int B, int T, int H) {
+  const long nkb = (T + attn::kKvBlk - 1) / attn::kKvBlk;
+  return nkb * B * H * (long)T * attn::kHD;
+}
+
 hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse, void* dqkv,
-                           float* delta, float* dq_accum, int B, int T, int H, hipStream_t stream) {
+                           float* delta, float* dq_part, int B, int T, int H, hipStream_t stream) {
   if (B <= 0 || T <= 0 || H <= 0) return hipErrorInvalidValue;
   const long rows = (long)B * T * H;
-  hipError_t e = hipMemsetAsync(dq_accum, 0, rows * attn::kHD * sizeof(float), stream);
-  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, stream,
                      (const bf16_raw*)dout, (const bf16_raw*)out, delta, T, H, rows);
   const int nkb = (T + attn::kKvBlk - 1) / attn::kKvBlk;
-  static const bool no_dq = [] {
-    const char* e = getenv("LLMT_EXPERIMENT");
-    return e != nullptr && strcmp(e, "attn_no_dq") == 0;
-  }();
-  auto kern = no_dq ? attn::attn_bwd_kernel<false> : attn::attn_bwd_kernel<true>;
-  hipLaunchKernelGGL(kern, dim3(B * H, nkb), dim3(512), 0, stream, (const bf16_raw*)qkv,
-                     (const bf16_raw*)dout, lse, delta, (bf16_raw*)dqkv, dq_accum, T, H, nkb);
+  hipLaunchKernelGGL(attn::attn_bwd_kernel, dim3(B * H, nkb), dim3(512), 0, stream, (const bf16_raw*)qkv,
+                     (const bf16_raw*)dout, lse, delta, (bf16_raw*)dqkv, dq_part, T, H, nkb);
   const long n8 = rows * attn::kHD / 8;
-  hipLaunchKernelGGL(attn::attn_dq_store_kernel, dim3((n8 + 255) / 256), dim3(256), 0, stream, dq_accum,
-                     (bf16_raw*)dqkv, H, n8);
+  hipLaunchKernelGGL(attn::attn_dq_reduce_kernel, dim3((n8 + 255) / 256), dim3(256), 0, stream, dq_part,
+                     (bf16_raw*)dqkv, T, H, nkb, n8);
   return hipGetLastError();
 }
 

@@ -280,7 +280,7 @@ Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const 
   at::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
   Tensor dqkv = at::empty_like(qkv);
   Tensor delta = at::empty({B, H, T}, lse.options());
-  Tensor dq = at::empty({B * T * H * 64}, lse.options());
+  Tensor dq = at::empty({llmt::attn_bwd_workspace_floats((int)B, (int)T, (int)H)}, lse.options());
   check_hip(llmt::launch_attn_bwd(dout.data_ptr(), qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
                                   dqkv.data_ptr(), delta.data_ptr<float>(), dq.data_ptr<float>(), (int)B, (int)T,
                                   (int)H, cur_stream()),

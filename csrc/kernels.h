@@ -96,9 +96,11 @@ hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, fl
 // lse [B, H, T] f32 (natural-log normaliser).
 hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H,
                            hipStream_t stream);
-// dqkv [B, T, 3, H, 64] bf16; `delta` [B, H, T] f32 and `dq_accum` [B, T, H, 64] f32 scratch
+// dqkv [B, T, 3, H, 64] bf16; `delta` [B, H, T] f32 and `dq_part`
+// (attn_bwd_workspace_floats(B, T, H) floats) scratch
+long attn_bwd_workspace_floats(int B, int T, int H);
 hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse,
-                           void* dqkv, float* delta, float* dq_accum, int B, int T, int H,
+                           void* dqkv, float* delta, float* dq_part, int B, int T, int H,
                            hipStream_t stream);
 
 }  // namespace llmt

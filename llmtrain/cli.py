@@ -3,6 +3,10 @@
 ``llmtrain [-v] [--version] {train,validate,print-config} --config PATH [--run-id ID]
 [--dry-run] [--json] [--resume RUN_ID|DIR|FILE]``
 
+``llmtrain generate --config PATH [--checkpoint RUN_ID|DIR|FILE] --prompt TEXT ...`` samples
+from a trained ``gpt`` checkpoint with the KV-cached sampler of :mod:`llmtrain.inference` (the
+reference has this only as notebook code, notebooks/trained_vs_random_completion.ipynb).
+
 Exit codes: 0 success, 2 config/registry error, 1 training or dry-run failure.  Only rank 0
 creates the run directory, writes ``config.yaml``/``meta.json``, owns a real tracker and prints
 the summary.  In ``--json`` mode every logger used during the run writes to stderr so stdout
@@ -135,6 +139,19 @@ def build_parser() -> argparse.ArgumentParser:
     train.add_argument("--resume", default=None, help="Resume from a run_id, checkpoint dir or .pt file.")
     sub.add_parser("validate", parents=[common], help="Validate a config file.")
     sub.add_parser("print-config", parents=[common], help="Print the resolved config with defaults.")
+    gen = sub.add_parser("generate", help="Sample text from a trained gpt checkpoint (KV-cached).")
+    gen.add_argument("--config", required=True, help="Path to the YAML configuration file.")
+    gen.add_argument("--json", action="store_true", help="Emit machine-readable JSON output.")
+    gen.add_argument("--checkpoint", default=None,
+                     help="run_id, run/checkpoints dir or step_*.pt (omit: random-init weights).")
+    gen.add_argument("--prompt", action="append", required=True, help="Prompt text (repeatable).")
+    gen.add_argument("--max-new-tokens", type=int, default=48)
+    gen.add_argument("--temperature", type=float, default=0.8, help="<= 0 means greedy argmax.")
+    gen.add_argument("--top-k", type=int, default=40, help="0 disables the top-k cutoff.")
+    gen.add_argument("--seed", type=int, default=1234)
+    gen.add_argument("--top-next", type=int, default=0, help="Also list the k most likely next tokens.")
+    gen.add_argument("--device", default=None, help="Override run.device (cpu | cuda).")
+    gen.add_argument("--no-cache", action="store_true", help="Recompute the full context every step.")
     return parser
 
 
@@ -253,9 +270,91 @@ def _handle_train(args: argparse.Namespace) -> int:
     return 0
 
 
+def _resolve_checkpoint(spec: str, root_dir: str) -> Path:
+    """A ``.pt`` file, a directory holding ``step_*.pt`` (or its run dir), or a run_id under
+    ``output.root_dir`` — the same forms ``train --resume`` accepts."""
+    from llmtrain.training.checkpoint import CheckpointManager
+
+    path = Path(spec)
+    if path.is_file():
+        return path
+    candidates = [path, path / "checkpoints"] if path.is_dir() else [Path(root_dir) / spec / "checkpoints"]
+    for cand in candidates:
+        if cand.is_dir():
+            latest = CheckpointManager(cand).latest_checkpoint()
+            if latest is not None:
+                return latest
+    raise FileNotFoundError(f"no checkpoint found for {spec!r}")
+
+
+def _handle_generate(args: argparse.Namespace) -> int:
+    args.verbose = getattr(args, "verbose", 0)
+    config = _load(args)
+    if config is None:
+        return 2
+    import torch
+
+    from llmtrain.inference import generate_text, top_next_tokens
+    from llmtrain.models.gpt import GPT
+    from llmtrain.runtime.device import seed_everything
+    from llmtrain.training.checkpoint import CheckpointManager
+
+    initialize_registries()
+    try:
+        adapter = get_model_adapter(config.model.name)()
+    except RegistryError as exc:
+        print(f"Registry error: {exc}", file=sys.stderr)
+        return 2
+    try:
+        seed_everything(config.run.seed)
+        model = adapter.build_model(config)
+        if not isinstance(model, GPT):
+            print(f"generate supports the causal 'gpt' model, not {config.model.name!r}", file=sys.stderr)
+            return 2
+        tokenizer = adapter.build_tokenizer(config)
+        source = "random-init"
+        if args.checkpoint:
+            ckpt = _resolve_checkpoint(args.checkpoint, config.output.root_dir)
+            payload = CheckpointManager(ckpt.parent).load(ckpt)
+            model.load_state_dict(payload["model_state_dict"])
+            source = str(ckpt)
+        want = args.device or config.run.device
+        device = torch.device("cuda" if want in ("cuda", "rocm") and torch.cuda.is_available() else "cpu")
+        model = model.to(device).eval()
+        results: list[dict[str, Any]] = []
+        for prompt in args.prompt:
+            ids = tokenizer.encode(prompt)
+            if not ids or max(ids) >= model.vocab_size:
+                raise ValueError(f"prompt {prompt!r} encodes to no tokens or to ids >= vocab_size {model.vocab_size}")
+            text = generate_text(
+                model, tokenizer, prompt, max_new_tokens=args.max_new_tokens, temperature=args.temperature,
+                top_k=args.top_k if args.top_k > 0 else None, seed=args.seed, use_cache=not args.no_cache,
+            )
+            entry: dict[str, Any] = {"prompt": prompt, "completion": text}
+            if args.top_next > 0:
+                entry["top_next"] = [[tok, p] for tok, p in top_next_tokens(model, tokenizer, prompt, k=args.top_next)]
+            results.append(entry)
+    except Exception as exc:  # noqa: BLE001 - CLI boundary: report and exit 1
+        print(f"Generation failed: {exc}", file=sys.stderr)
+        return 1
+    if args.json:
+        print(json.dumps({"checkpoint": source, "device": str(device), "results": results}, indent=2))
+    else:
+        for entry in results:
+            print(f"=== prompt ===\n{entry['prompt']}\n=== completion ({source}) ===\n{entry['completion']}")
+            for tok, p in entry.get("top_next", []):
+                print(f"{tok!r}: {p:.4f}")
+    return 0
+
+
 def main(argv: Sequence[str] | None = None) -> int:
     args = build_parser().parse_args(argv)
-    handlers = {"validate": _handle_validate, "print-config": _handle_print_config, "train": _handle_train}
+    handlers = {
+        "validate": _handle_validate,
+        "print-config": _handle_print_config,
+        "train": _handle_train,
+        "generate": _handle_generate,
+    }
     handler = handlers.get(args.command)
     if handler is None:
         print(f"Unknown command: {args.command}", file=sys.stderr)

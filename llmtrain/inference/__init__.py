@@ -1,0 +1,12 @@
+"""Inference: KV-cached autoregressive sampling for the ``gpt`` model."""
+
+from llmtrain.inference.generate import (
+    KVCache,
+    forward_cached,
+    generate,
+    generate_text,
+    sample_next_token,
+    top_next_tokens,
+)
+
+__all__ = ["KVCache", "forward_cached", "generate", "generate_text", "sample_next_token", "top_next_tokens"]

@@ -3,8 +3,10 @@ PY ?= python
 NPROC ?= 8
 GPURUN ?= /usr/local/graft/bin/gpurun
 
-.PHONY: build test test-gpu bench bench-module profile train-smoke train-ddp train-gpt2 train-gpt2-ddp8 \
-        k8s-build k8s-train k8s-logs k8s-clean k8s-e2e lint
+.PHONY: build test test-gpu bench bench-module profile parity train-smoke train-ddp train-gpt2 train-gpt2-ddp8 \
+        generate mlflow k8s-build k8s-train k8s-logs k8s-clean k8s-e2e lint \
+        k8s-kind-cluster k8s-kind-delete k8s-kind-smoke k8s-mlflow \
+        k8s-dashboard k8s-dashboard-token k8s-dashboard-proxy k8s-dashboard-delete
 
 build:                 ## compile every HIP kernel for gfx950 into llmtrain/ops/_llmtrain_hip.so
 	$(PY) -m llmtrain.ops.build
@@ -23,6 +25,16 @@ bench-module:          ## same benchmark through plain PyTorch (autocast + SDPA)
 
 profile: build         ## rocprofv3 kernel trace + per-kernel stats of the bench
 	bash scripts/profile.sh
+
+parity: build          ## val-loss parity: fused engine vs torch bf16 vs fp32 oracle (one GPU)
+	$(PY) bench/parity.py --steps 300
+
+generate:              ## sample from the newest checkpoint of a run: make generate RUN=<run_id> PROMPT="..."
+	$(PY) -m llmtrain generate --config $(or $(CONFIG),configs/presets/gpt2_124m_mi355x.yaml) \
+	  --checkpoint $(RUN) --prompt "$(or $(PROMPT),Hello)" --top-next 5
+
+mlflow:                ## MLflow UI over the local SQLite store
+	mlflow ui --backend-store-uri sqlite:///./mlflow.db
 
 train-smoke:
 	$(PY) -m llmtrain train --config configs/presets/gpt_smoke.yaml
@@ -51,3 +63,37 @@ k8s-clean:
 
 k8s-e2e:
 	bash k8s/test_e2e.sh
+
+# ---- local kind cluster: CPU smoke of the same IndexedJob plumbing (gloo, 2 pods) -------------
+DASHBOARD_URL ?= https://raw.githubusercontent.com/kubernetes/dashboard/v2.7.0/aio/deploy/recommended.yaml
+
+k8s-kind-cluster:
+	mkdir -p runs mlflow-k8s
+	kind create cluster --name llmtrain --config k8s/kind/kind-config.yaml
+
+k8s-kind-delete:
+	kind delete cluster --name llmtrain
+
+k8s-kind-smoke: k8s-build
+	kind load docker-image llmtrain-mi355x:dev --name llmtrain
+	kubectl apply -f k8s/rbac.yaml -f k8s/storage.yaml -f k8s/kind/configmap-cpu.yaml -f k8s/service.yaml -f k8s/kind/job-cpu.yaml
+	kubectl wait --for=condition=complete --timeout=600s job/llmtrain
+
+k8s-mlflow:
+	mlflow ui --backend-store-uri sqlite:///mlflow-k8s/mlflow.db
+
+k8s-dashboard:
+	kubectl apply -f $(DASHBOARD_URL)
+	kubectl apply -f k8s/dashboard-admin.yaml
+	@$(MAKE) --no-print-directory k8s-dashboard-token
+	@echo "then: make k8s-dashboard-proxy and open http://localhost:8001/api/v1/namespaces/kubernetes-dashboard/services/https:kubernetes-dashboard:/proxy/"
+
+k8s-dashboard-token:
+	@kubectl -n kubernetes-dashboard create token llmtrain-dashboard-admin
+
+k8s-dashboard-proxy:
+	kubectl proxy
+
+k8s-dashboard-delete:
+	kubectl delete -f k8s/dashboard-admin.yaml --ignore-not-found
+	kubectl delete -f $(DASHBOARD_URL) --ignore-not-found

@@ -38,7 +38,7 @@ MODELS = {
 def make_config(args: argparse.Namespace, world: int):
     from llmtrain.config.schemas import RunConfig
 
-    model = dict(MODELS[args.model], name="gpt", dropout=0.0, tie_embeddings=True)
+    model = dict(MODELS[args.model], name="gpt", dropout=args.dropout, tie_embeddings=True)
     if args.path == "module":
         model["extra"] = {"fused": False}
     payload = {
@@ -78,6 +78,7 @@ def main() -> int:
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--path", choices=["fused", "module"], default="fused")
+    ap.add_argument("--dropout", type=float, default=0.0, help="model dropout (reference default 0.1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -148,6 +149,7 @@ def main() -> int:
                 "micro_batch_per_gpu": cfg.trainer.micro_batch_size,
                 "grad_accum": cfg.trainer.grad_accum_steps,
                 "path": args.path,
+                "dropout": args.dropout,
             },
             "tokens_per_sec_per_gpu": round(tps / world, 1),
             "mfu": round(mfu(tps / world, per_tok), 4),

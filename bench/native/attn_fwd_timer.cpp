@@ -1,0 +1,59 @@
+// Stand-alone timer for attention-forward A/B experiments (see attn_bwd_timer.cpp): links ONE
+// object defining llmt::launch_attn_fwd and times it on GPT-2 124M's attention shape.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "kernels.h"
+
+#define CHECK(x)                                                                     \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      std::exit(1);                                                                  \
+    }                                                                                \
+  } while (0)
+
+int main(int argc, char** argv) {
+  const int B = argc > 1 ? std::atoi(argv[1]) : 32, T = 1024, H = 12, D = 64;
+  const size_t nqkv = (size_t)B * T * 3 * H * D, nout = (size_t)B * T * H * D, nrow = (size_t)B * H * T;
+  std::vector<unsigned short> h(nqkv);
+  unsigned s = 12345;
+  for (auto& v : h) {
+    s = s * 1664525u + 1013904223u;
+    const float f = (((s >> 9) & 0xffff) / 65536.0f - 0.5f) * 4.0f;
+    unsigned u;
+    std::memcpy(&u, &f, 4);
+    v = (unsigned short)(u >> 16);
+  }
+  void *qkv, *out;
+  float* lse;
+  CHECK(hipMalloc(&qkv, nqkv * 2));
+  CHECK(hipMalloc(&out, nout * 2));
+  CHECK(hipMalloc(&lse, nrow * 4));
+  CHECK(hipMemcpy(qkv, h.data(), nqkv * 2, hipMemcpyHostToDevice));
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  for (int i = 0; i < 5; ++i) CHECK(llmt::launch_attn_fwd(qkv, out, lse, B, T, H, 0));
+  std::vector<float> ms;
+  for (int i = 0; i < 30; ++i) {
+    CHECK(hipEventRecord(a, 0));
+    CHECK(llmt::launch_attn_fwd(qkv, out, lse, B, T, H, 0));
+    CHECK(hipEventRecord(b, 0));
+    CHECK(hipEventSynchronize(b));
+    float t;
+    CHECK(hipEventElapsedTime(&t, a, b));
+    ms.push_back(t);
+  }
+  std::sort(ms.begin(), ms.end());
+  const double flops = 4.0 * B * H * (double)T * T * D / 2;
+  std::printf("{\"kernel\": \"attn_fwd\", \"variant\": \"%s\", \"B\": %d, \"ms\": %.4f, \"TFLOPs\": %.1f}\n",
+              argc > 2 ? argv[2] : "?", B, ms[ms.size() / 2], flops / ms[ms.size() / 2] / 1e9);
+  return 0;
+}

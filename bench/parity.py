@@ -45,7 +45,7 @@ def run_path(path: str, args: argparse.Namespace) -> dict:
     from llmtrain.config.schemas import RunConfig
     from llmtrain.training.trainer import Trainer
 
-    model = dict(MODELS[args.model], name="gpt", dropout=0.0, tie_embeddings=True)
+    model = dict(MODELS[args.model], name="gpt", dropout=args.dropout, tie_embeddings=True)
     fused = path == "fused"
     model["extra"] = {"fused": fused}
     precision = "fp32" if path == "module_fp32" else "bf16"
@@ -98,6 +98,8 @@ def main() -> int:
     ap.add_argument("--lr", type=float, default=3e-4)
     ap.add_argument("--warmup", type=int, default=None, help="LR warm-up steps (default: steps // 3)")
     ap.add_argument("--seed", type=int, default=1337)
+    ap.add_argument("--dropout", type=float, default=0.0,
+                    help="model dropout; > 0 compares the fused masks with torch's dropout statistically")
     ap.add_argument("--paths", default="fused,module_bf16,module_fp32")
     ap.add_argument("--trajectory", type=int, default=0, help="print per-step losses/grad norms of N steps instead")
     args = ap.parse_args()
@@ -113,7 +115,7 @@ def main() -> int:
     if args.trajectory:
         return 0
     oracle = next((r for r in rows if r["path"] == "module_fp32"), None)
-    summary: dict = {"model": args.model, "steps": args.steps, "micro_batch": args.micro_batch,
+    summary: dict = {"model": args.model, "steps": args.steps, "micro_batch": args.micro_batch, "dropout": args.dropout,
                      "tokens": args.steps * args.micro_batch * MODELS[args.model]["block_size"]}
     if oracle and oracle["val_loss"]:
         for r in rows:

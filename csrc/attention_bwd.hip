@@ -100,12 +100,14 @@ __device__ __forceinline__ float buf_load_f32(__amdgpu_buffer_rsrc_t r, int byte
 // 16 rows a ds_read_b128 lane group touches land on 16 distinct chunks (all 64 banks)
 __device__ __forceinline__ int kt_off(int d, int key) { return d * kKvBlk + ((((key >> 3) ^ (d & 15))) << 3) + (key & 7); }
 
+template <bool DROPOUT>
 __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __restrict__ qkv,
                                                           const bf16_raw* __restrict__ dout,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta,
                                                           bf16_raw* __restrict__ dqkv,
-                                                          float* __restrict__ dq_part, int T, int H, int nkb) {
+                                                          float* __restrict__ dq_part, int T, int H, int nkb,
+                                                          DropoutArgs dr) {
   __shared__ __attribute__((aligned(16))) bf16_raw kt_lds[kHD * kKvBlk];             // K^T, 32 KB
   __shared__ __attribute__((aligned(16))) bf16_raw qd_lds[2][2][kQTile * kHD];      // [buf][Q|dO] 32 KB
   __shared__ __attribute__((aligned(16))) bf16_raw ds_lds[2][kKvBlk * kQTile];      // [buf][key][q] 64 KB
@@ -115,7 +117,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int half = lane >> 5, col = lane & 31;
   const int bh = blockIdx.x;                 // all key blocks of one (b, h) share an XCD
-  const int kb = nkb - 1 - (int)blockIdx.y;  // ... and the heaviest (first) key blocks go first
+  const int kb = (int)blockIdx.y;            // ... and the heaviest key blocks (most query tiles) go first
   const int b = bh / H, h = bh - b * H;
   const long row_stride = 3L * H * kHD;
   const bf16_raw* base = qkv + (long)b * T * row_stride + (long)h * kHD;
@@ -131,6 +133,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   const __amdgpu_buffer_rsrc_t r_lse = __builtin_amdgcn_make_buffer_rsrc((void*)lse_bh, (short)0, T * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t r_del = __builtin_amdgcn_make_buffer_rsrc((void*)delta_bh, (short)0, T * 4, 0x00020000);
 
+  const uint32_t pseed = DROPOUT ? mix32(dr.seed + (uint32_t)bh * 0x9E3779B9u) : 0u;  // see attn fwd
   const int kblk0 = kb * kKvBlk;
   const int kw0 = kblk0 + 32 * wave;  // first key of this wave
   const int key = kw0 + col;          // this lane's key
@@ -210,6 +213,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
           dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[kk], dp, 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);  // row constants are read after the chains (VGPR budget)
+        float ddv[16];  // delta per row, kept only by the dropout variant
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const f32x4 l2 = *reinterpret_cast<const f32x4*>(&rowc[32 * qs + 8 * rr + 4 * half]);
@@ -217,7 +221,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             p[4 * rr + i] = __builtin_amdgcn_exp2f(fmaf(p[4 * rr + i], c, -l2[i]));
-            dp[4 * rr + i] -= dd[i];
+            if (DROPOUT) ddv[4 * rr + i] = dd[i];
+            else dp[4 * rr + i] -= dd[i];
           }
         }
         if (!full && ((kw0 + 31 > qb0) || (kw0 + 32 > T) || (qb0 + 32 > T))) {
@@ -230,8 +235,20 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
             p[r] = (roff < lo || roff > hi) ? 0.f : p[r];
           }
         }
+        if (DROPOUT) {
+          // dP above is the gradient of the DROPPED probabilities: undo the mask for dS, and feed
+          // dV the dropped P (element (q, key) of the plane: q*T + key, as in the forward)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) ds[r] = p[r] * dp[r];
+          for (int r = 0; r < 16; ++r) {
+            const uint32_t qq = (uint32_t)(qb0 + 4 * half + (r & 3) + 8 * (r >> 2));
+            const bool kp = drop_keep(pseed, dr.thr, qq * (uint32_t)T + (uint32_t)key);
+            ds[r] = p[r] * ((kp ? dp[r] * dr.scale : 0.f) - ddv[r]);
+            p[r] = kp ? p[r] * dr.scale : 0.f;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) ds[r] = p[r] * dp[r];
+        }
         // dV^T += dO^T P ; dK^T += Q^T dS  (P, dS used in place as B operands)
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
@@ -345,14 +362,19 @@ long attn_bwd_workspace_floats(int B, int T, int H) {
 }
 
 hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse, void* dqkv,
-                           float* delta, float* dq_part, int B, int T, int H, hipStream_t stream) {
-  if (B <= 0 || T <= 0 || H <= 0) return hipErrorInvalidValue;
+                           float* delta, float* dq_part, int B, int T, int H, DropoutArgs dropout,
+                           hipStream_t stream) {
+  if (B <= 0 || T <= 0 || H <= 0 || T > 65535) return hipErrorInvalidValue;
   const long rows = (long)B * T * H;
   hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, stream,
                      (const bf16_raw*)dout, (const bf16_raw*)out, delta, T, H, rows);
   const int nkb = (T + attn::kKvBlk - 1) / attn::kKvBlk;
-  hipLaunchKernelGGL(attn::attn_bwd_kernel, dim3(B * H, nkb), dim3(512), 0, stream, (const bf16_raw*)qkv,
-                     (const bf16_raw*)dout, lse, delta, (bf16_raw*)dqkv, dq_part, T, H, nkb);
+  if (dropout.thr != 0)
+    hipLaunchKernelGGL(attn::attn_bwd_kernel<true>, dim3(B * H, nkb), dim3(512), 0, stream, (const bf16_raw*)qkv,
+                       (const bf16_raw*)dout, lse, delta, (bf16_raw*)dqkv, dq_part, T, H, nkb, dropout);
+  else
+    hipLaunchKernelGGL(attn::attn_bwd_kernel<false>, dim3(B * H, nkb), dim3(512), 0, stream, (const bf16_raw*)qkv,
+                       (const bf16_raw*)dout, lse, delta, (bf16_raw*)dqkv, dq_part, T, H, nkb, dropout);
   const long n8 = rows * attn::kHD / 8;
   hipLaunchKernelGGL(attn::attn_dq_reduce_kernel, dim3((n8 + 255) / 256), dim3(256), 0, stream, dq_part,
                      (bf16_raw*)dqkv, T, H, nkb, n8);

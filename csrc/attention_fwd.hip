@@ -30,10 +30,11 @@ constexpr int kFwdWaves = 4;
 constexpr int kQBlk = 32 * kFwdWaves;  // 128 query rows per workgroup
 constexpr int kKBlk = 64;              // keys per LDS tile
 
+template <bool DROPOUT>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __restrict__ qkv,
                                                           bf16_raw* __restrict__ out,
                                                           float* __restrict__ lse, int T, int H,
-                                                          int nqb) {
+                                                          int nqb, DropoutArgs dr) {
   __shared__ __attribute__((aligned(16))) bf16_raw smem[2][2][kKBlk * kHD];  // [buf][K|V][tile]
   const int lane = threadIdx.x & 63;
   // readfirstlane makes the wave index (and every tile/mask decision derived from it) provably
@@ -45,6 +46,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
   const int b = bh / H, h = bh - b * H;
   const long row_stride = 3L * H * kHD;  // elements between consecutive tokens in qkv
   const bf16_raw* base = qkv + (long)b * T * row_stride + (long)h * kHD;
+  // attention-probability dropout: plane seed per (b, h), element index q*T + key
+  const uint32_t pseed = DROPOUT ? mix32(dr.seed + (uint32_t)bh * 0x9E3779B9u) : 0u;
 
   const int q0w = qb * kQBlk + wave * 32;   // first query row of this wave
   const int q = q0w + col;                   // this lane's query row
@@ -151,6 +154,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
         }
       }
       psum += __shfl_xor(psum, 32, 64);
+      if (DROPOUT) {  // the normaliser sums the undropped P; P V uses the masked, rescaled P
+        const uint32_t e_q = (uint32_t)q * (uint32_t)T + (uint32_t)(kbase + 4 * half);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const uint32_t e = e_q + (uint32_t)(kt * 32 + (r & 3) + 8 * (r >> 2));
+            s[kt][r] = drop_keep(pseed, dr.thr, e) ? s[kt][r] * dr.scale : 0.f;
+          }
+      }
       l_run = l_run * alpha + psum;
       m_run = m_new;
       o[0] *= alpha;
@@ -192,12 +205,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
 
 }  // namespace attn
 
-hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H, hipStream_t stream) {
-  if (B <= 0 || T <= 0 || H <= 0) return hipErrorInvalidValue;
+hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H, DropoutArgs dropout,
+                           hipStream_t stream) {
+  if (B <= 0 || T <= 0 || H <= 0 || T > 65535) return hipErrorInvalidValue;
   const int nqb = (T + attn::kQBlk - 1) / attn::kQBlk;
   dim3 grid(nqb, B * H);
-  hipLaunchKernelGGL(attn::attn_fwd_kernel, grid, dim3(256), 0, stream, (const bf16_raw*)qkv, (bf16_raw*)out, lse,
-                     T, H, nqb);
+  if (dropout.thr != 0)
+    hipLaunchKernelGGL(attn::attn_fwd_kernel<true>, grid, dim3(256), 0, stream, (const bf16_raw*)qkv, (bf16_raw*)out,
+                       lse, T, H, nqb, dropout);
+  else
+    hipLaunchKernelGGL(attn::attn_fwd_kernel<false>, grid, dim3(256), 0, stream, (const bf16_raw*)qkv, (bf16_raw*)out,
+                       lse, T, H, nqb, dropout);
   return hipGetLastError();
 }
 

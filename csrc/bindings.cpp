@@ -39,10 +39,24 @@ bool is_lowp(const Tensor& t, const char* name) {
   return t.scalar_type() == at::kBFloat16;
 }
 
+// dropout probability + site seed -> kernel arguments (thr = round(p * 2^16); the scale uses the
+// quantised keep probability so the mask stays unbiased)
+llmt::DropoutArgs make_dropout(double p, int64_t seed) {
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout p must be in [0, 1)");
+  llmt::DropoutArgs d{};
+  const uint32_t thr = (uint32_t)std::lround(p * 65536.0);
+  if (thr == 0) return d;
+  d.seed = (uint32_t)(seed & 0xffffffffLL);
+  d.thr = thr > 65535u ? 65535u : thr;
+  d.scale = 65536.0f / (float)(65536u - d.thr);
+  return d;
+}
+
 // ---- LayerNorm -----------------------------------------------------------------------------
 std::tuple<Tensor, Tensor, Tensor, Tensor> add_layernorm_fwd(const Tensor& x, const c10::optional<Tensor>& delta,
                                                              const Tensor& w, const Tensor& b, double eps,
-                                                             at::ScalarType out_dtype) {
+                                                             at::ScalarType out_dtype, double dropout_p,
+                                                             int64_t dropout_seed) {
   check_gpu(x, "x");
   check_dtype(x, at::kFloat, "x");
   check_gpu(w, "weight");
@@ -80,6 +94,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> add_layernorm_fwd(const Tensor& x, co
   a.M = (int)M;
   a.d = (int)d;
   a.eps = (float)eps;
+  a.dropout = make_dropout(dropout_p, dropout_seed);
   if (M > 0) check_hip(llmt::launch_add_layernorm_fwd(a, cur_stream()), "add_layernorm_fwd");
   return {xs, y, mean, rstd};
 }
@@ -87,7 +102,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> add_layernorm_fwd(const Tensor& x, co
 std::tuple<Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor& xs, const Tensor& mean, const Tensor& rstd,
                                          const Tensor& w, const c10::optional<Tensor>& dresid, Tensor dw, Tensor db,
                                          const c10::optional<Tensor>& dy_scale, bool want_lowp,
-                                         const c10::optional<Tensor>& dproj) {
+                                         const c10::optional<Tensor>& dproj, double dropout_p, int64_t dropout_seed) {
   check_gpu(dy, "dy");
   check_gpu(xs, "xs");
   check_dtype(xs, at::kFloat, "xs");
@@ -138,6 +153,7 @@ std::tuple<Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor& xs, con
   }
   a.M = (int)M;
   a.d = (int)d;
+  a.dropout = make_dropout(dropout_p, dropout_seed);
   if (M > 0) check_hip(llmt::launch_layernorm_bwd(a, cur_stream()), "layernorm_bwd");
   return {dx, dx_lp};
 }
@@ -210,7 +226,7 @@ void colsum_accum(const Tensor& dy, Tensor out) {
               "colsum_accum");
 }
 
-Tensor embedding_fwd(const Tensor& ids, const Tensor& wte, const Tensor& wpe) {
+Tensor embedding_fwd(const Tensor& ids, const Tensor& wte, const Tensor& wpe, double dropout_p, int64_t dropout_seed) {
   check_gpu(ids, "ids");
   check_gpu(wte, "wte");
   check_gpu(wpe, "wpe");
@@ -224,12 +240,14 @@ Tensor embedding_fwd(const Tensor& ids, const Tensor& wte, const Tensor& wpe) {
   Tensor x = at::empty({B * T, d}, wte.options());
   if (B * T > 0)
     check_hip(llmt::launch_embedding_fwd(ids.data_ptr<int64_t>(), wte.data_ptr<float>(), wpe.data_ptr<float>(),
-                                         x.data_ptr<float>(), (int)B, (int)T, (int)d, (int)wte.size(0), cur_stream()),
+                                         x.data_ptr<float>(), (int)B, (int)T, (int)d, (int)wte.size(0),
+                                         make_dropout(dropout_p, dropout_seed), cur_stream()),
               "embedding_fwd");
   return x;
 }
 
-void embedding_bwd(const Tensor& dx, const Tensor& ids, Tensor dwte, Tensor dwpe) {
+void embedding_bwd(const Tensor& dx, const Tensor& ids, Tensor dwte, Tensor dwpe, double dropout_p,
+                   int64_t dropout_seed) {
   check_gpu(dx, "dx");
   check_gpu(ids, "ids");
   check_gpu(dwte, "dwte");
@@ -244,7 +262,7 @@ void embedding_bwd(const Tensor& dx, const Tensor& ids, Tensor dwte, Tensor dwpe
   if (B * T > 0)
     check_hip(llmt::launch_embedding_bwd(dx.data_ptr<float>(), ids.data_ptr<int64_t>(), dwte.data_ptr<float>(),
                                          dwpe.data_ptr<float>(), (int)B, (int)T, (int)d, (int)dwte.size(0),
-                                         cur_stream()),
+                                         make_dropout(dropout_p, dropout_seed), cur_stream()),
               "embedding_bwd");
 }
 
@@ -255,19 +273,20 @@ void check_qkv(const Tensor& qkv, int64_t B, int64_t T, int64_t H) {
   TORCH_CHECK(qkv.numel() == B * T * 3 * H * 64, "qkv must be [B*T, 3*H*64] (head_dim 64 only)");
 }
 
-std::tuple<Tensor, Tensor> attn_fwd(const Tensor& qkv, int64_t B, int64_t T, int64_t H) {
+std::tuple<Tensor, Tensor> attn_fwd(const Tensor& qkv, int64_t B, int64_t T, int64_t H, double dropout_p,
+                                    int64_t dropout_seed) {
   check_qkv(qkv, B, T, H);
   at::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
   Tensor out = at::empty({B * T, H * 64}, qkv.options());
   Tensor lse = at::empty({B, H, T}, qkv.options().dtype(at::kFloat));
   check_hip(llmt::launch_attn_fwd(qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(), (int)B, (int)T, (int)H,
-                                  cur_stream()),
+                                  make_dropout(dropout_p, dropout_seed), cur_stream()),
             "attn_fwd");
   return {out, lse};
 }
 
 Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const Tensor& lse, int64_t B, int64_t T,
-                int64_t H) {
+                int64_t H, double dropout_p, int64_t dropout_seed) {
   check_qkv(qkv, B, T, H);
   for (const Tensor* t : {&dout, &out}) {
     check_gpu(*t, "dout/out");
@@ -283,9 +302,19 @@ Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const 
   Tensor dq = at::empty({llmt::attn_bwd_workspace_floats((int)B, (int)T, (int)H)}, lse.options());
   check_hip(llmt::launch_attn_bwd(dout.data_ptr(), qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
                                   dqkv.data_ptr(), delta.data_ptr<float>(), dq.data_ptr<float>(), (int)B, (int)T,
-                                  (int)H, cur_stream()),
+                                  (int)H, make_dropout(dropout_p, dropout_seed), cur_stream()),
             "attn_bwd");
   return dqkv;
+}
+
+// keep-mask of `n` consecutive elements of one dropout site (tests / debugging)
+Tensor dropout_mask(int64_t n, double p, int64_t seed, const Tensor& like) {
+  check_gpu(like, "like");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(like.device());
+  Tensor m = at::empty({n}, like.options().dtype(at::kBool));
+  if (n > 0)
+    check_hip(llmt::launch_dropout_mask(make_dropout(p, seed), (bool*)m.data_ptr(), n, cur_stream()), "dropout_mask");
+  return m;
 }
 
 // ---- weight-gradient GEMM --------------------------------------------------------------------
@@ -358,19 +387,22 @@ void adamw_flat(Tensor param, const Tensor& grad, Tensor exp_avg, Tensor exp_avg
 }  // namespace
 
 TORCH_LIBRARY(llmtrain_hip, m) {
-  m.def("add_layernorm_fwd(Tensor x, Tensor? delta, Tensor weight, Tensor bias, float eps, ScalarType out_dtype)"
-        " -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("add_layernorm_fwd(Tensor x, Tensor? delta, Tensor weight, Tensor bias, float eps, ScalarType out_dtype,"
+        " float dropout_p=0., int dropout_seed=0) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("layernorm_bwd(Tensor dy, Tensor xs, Tensor mean, Tensor rstd, Tensor weight, Tensor? dresid,"
-        " Tensor(a!) dweight, Tensor(b!) dbias, Tensor? dy_scale, bool want_lowp, Tensor(c!)? dproj_bias)"
-        " -> (Tensor, Tensor)");
+        " Tensor(a!) dweight, Tensor(b!) dbias, Tensor? dy_scale, bool want_lowp, Tensor(c!)? dproj_bias,"
+        " float dropout_p=0., int dropout_seed=0) -> (Tensor, Tensor)");
   m.def("cross_entropy_fwd_bwd(Tensor(a!) logits, Tensor labels, int vocab, Tensor row_weight) -> Tensor");
   m.def("gelu_fwd(Tensor u) -> Tensor");
   m.def("gelu_bwd(Tensor dg, Tensor u, Tensor(a!)? dbias) -> Tensor");
   m.def("colsum_accum(Tensor dy, Tensor(a!) out) -> ()");
-  m.def("embedding_fwd(Tensor ids, Tensor wte, Tensor wpe) -> Tensor");
-  m.def("embedding_bwd(Tensor dx, Tensor ids, Tensor(a!) dwte, Tensor(b!) dwpe) -> ()");
-  m.def("attn_fwd(Tensor qkv, int B, int T, int H) -> (Tensor, Tensor)");
-  m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, int B, int T, int H) -> Tensor");
+  m.def("embedding_fwd(Tensor ids, Tensor wte, Tensor wpe, float dropout_p=0., int dropout_seed=0) -> Tensor");
+  m.def("embedding_bwd(Tensor dx, Tensor ids, Tensor(a!) dwte, Tensor(b!) dwpe, float dropout_p=0.,"
+        " int dropout_seed=0) -> ()");
+  m.def("attn_fwd(Tensor qkv, int B, int T, int H, float dropout_p=0., int dropout_seed=0) -> (Tensor, Tensor)");
+  m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, int B, int T, int H, float dropout_p=0.,"
+        " int dropout_seed=0) -> Tensor");
+  m.def("dropout_mask(int n, float p, int seed, Tensor like) -> Tensor");
   m.def("wgrad_gemm(Tensor dy, Tensor x, Tensor(a!) c, int split=0, int tile=0) -> ()");
   m.def("sumsq(Tensor x) -> Tensor");
   m.def("adamw_flat(Tensor(a!) param, Tensor grad, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor(d!)? shadow,"
@@ -388,6 +420,7 @@ TORCH_LIBRARY_IMPL(llmtrain_hip, CUDA, m) {
   m.impl("embedding_bwd", &embedding_bwd);
   m.impl("attn_fwd", &attn_fwd);
   m.impl("attn_bwd", &attn_bwd);
+  m.impl("dropout_mask", &dropout_mask);
   m.impl("wgrad_gemm", &wgrad_gemm);
   m.impl("sumsq", &sumsq);
   m.impl("adamw_flat", &adamw_flat);

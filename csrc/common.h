@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "kernels.h"  // DropoutArgs
+
 namespace llmt {
 
 constexpr int kWave = 64;
@@ -38,6 +40,30 @@ __device__ __forceinline__ ushort8_t pack8(const float* f) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) v[i] = f2bf(f[i]);
   return v;
+}
+
+// ---- dropout masks ----------------------------------------------------------------------
+// Counter-based, so the backward regenerates the forward's mask instead of storing it.  Element e
+// of a site keeps iff its 16-bit uniform, half of h = mix32((e >> 1) ^ seed ^ hi * 0x85ebca6b)
+// (low half for even e, high half for odd e), is >= thr = round(p * 65536).  `seed` is already
+// mixed with the step seed and the site id on the host.  Bit-identical to
+// llmtrain/ops/reference.py (dropout_keep), which the CPU engine and the tests use.
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {  // "lowbias32" finaliser
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t drop_hash(uint32_t seed, uint64_t pair) {
+  return mix32((uint32_t)pair ^ seed ^ (uint32_t)(pair >> 32) * 0x85ebca6bu);
+}
+
+__device__ __forceinline__ bool drop_keep(uint32_t seed, uint32_t thr, uint64_t e) {
+  const uint32_t h = drop_hash(seed, e >> 1);
+  return ((e & 1) ? (h >> 16) : (h & 0xffffu)) >= thr;
 }
 
 template <typename T>

@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __res
                                                             const float* __restrict__ wte,
                                                             const float* __restrict__ wpe,
                                                             float* __restrict__ x, int M, int T,
-                                                            int d, int V) {
+                                                            int d, int V, DropoutArgs dr) {
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
   const int lane = threadIdx.x & 63;
@@ -111,7 +111,15 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __res
   const float4_t* e = reinterpret_cast<const float4_t*>(wte + tok * (long)d);
   const float4_t* p = reinterpret_cast<const float4_t*>(wpe + (long)t * d);
   float4_t* o = reinterpret_cast<float4_t*>(x + row * (long)d);
-  for (int c = lane; c < (d >> 2); c += 64) o[c] = e[c] + p[c];
+  for (int c = lane; c < (d >> 2); c += 64) {
+    float4_t v = e[c] + p[c];
+    if (dr.thr != 0) {  // embedding dropout (reference gpt.py:179 self.drop)
+      const uint64_t e0 = (uint64_t)row * d + 4 * c;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = drop_keep(dr.seed, dr.thr, e0 + k) ? v[k] * dr.scale : 0.f;
+    }
+    o[c] = v;
+  }
 }
 
 // dwte[ids[row]] += dx[row]: each wave adds one contiguous row (256-B wave segments, the
@@ -119,7 +127,7 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __res
 __global__ __launch_bounds__(256) void embedding_bwd_tok_kernel(const float* __restrict__ dx,
                                                                 const int64_t* __restrict__ ids,
                                                                 float* __restrict__ dwte, int M,
-                                                                int d, int V) {
+                                                                int d, int V, DropoutArgs dr) {
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
   const int lane = threadIdx.x & 63;
@@ -127,21 +135,38 @@ __global__ __launch_bounds__(256) void embedding_bwd_tok_kernel(const float* __r
   if (tok < 0 || tok >= V) return;
   const float* src = dx + row * (long)d;
   float* dst = dwte + tok * (long)d;
-  for (int c = lane; c < d; c += 64) atomicAdd(dst + c, src[c]);
+  for (int c = lane; c < d; c += 64) {
+    float g = src[c];
+    if (dr.thr != 0) g = drop_keep(dr.seed, dr.thr, (uint64_t)row * d + c) ? g * dr.scale : 0.f;
+    atomicAdd(dst + c, g);
+  }
 }
 
 // dwpe[t] += sum_b dx[b, t]: one thread per (t, float4 column chunk), no atomics.
 __global__ __launch_bounds__(256) void embedding_bwd_pos_kernel(const float* __restrict__ dx,
                                                                 float* __restrict__ dwpe, int B,
-                                                                int T, int d) {
+                                                                int T, int d, DropoutArgs dr) {
   const int d4 = d >> 2;
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long)T * d4) return;
   const int t = (int)(idx / d4), c = (int)(idx % d4);
   float4_t acc = {0.f, 0.f, 0.f, 0.f};
-  for (int b = 0; b < B; ++b)
-    acc += reinterpret_cast<const float4_t*>(dx + ((long)b * T + t) * d)[c];
+  for (int b = 0; b < B; ++b) {
+    const long row = (long)b * T + t;
+    float4_t g = reinterpret_cast<const float4_t*>(dx + row * d)[c];
+    if (dr.thr != 0) {
+      const uint64_t e0 = (uint64_t)row * d + 4 * c;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) g[k] = drop_keep(dr.seed, dr.thr, e0 + k) ? g[k] * dr.scale : 0.f;
+    }
+    acc += g;
+  }
   reinterpret_cast<float4_t*>(dwpe + (long)t * d)[c] += acc;
+}
+
+__global__ __launch_bounds__(256) void dropout_mask_kernel(DropoutArgs dr, bool* __restrict__ out, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = dr.thr == 0 || drop_keep(dr.seed, dr.thr, (uint64_t)i);
 }
 
 int rows_per_block_for(int M) {
@@ -185,20 +210,28 @@ hipError_t launch_colsum_accum(const void* dy, bool bf16, float* out, int M, int
 }
 
 hipError_t launch_embedding_fwd(const int64_t* ids, const float* wte, const float* wpe, float* x, int B,
-                                int T, int d, int V, hipStream_t stream) {
+                                int T, int d, int V, DropoutArgs dropout, hipStream_t stream) {
   if (d % 4 != 0) return hipErrorInvalidValue;
   const int M = B * T;
-  hipLaunchKernelGGL(embedding_fwd_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, ids, wte, wpe, x, M, T, d, V);
+  hipLaunchKernelGGL(embedding_fwd_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, ids, wte, wpe, x, M, T, d, V,
+                     dropout);
   return hipGetLastError();
 }
 
 hipError_t launch_embedding_bwd(const float* dx, const int64_t* ids, float* dwte, float* dwpe, int B, int T,
-                                int d, int V, hipStream_t stream) {
+                                int d, int V, DropoutArgs dropout, hipStream_t stream) {
   if (d % 4 != 0) return hipErrorInvalidValue;
   const int M = B * T;
-  hipLaunchKernelGGL(embedding_bwd_tok_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, dx, ids, dwte, M, d, V);
+  hipLaunchKernelGGL(embedding_bwd_tok_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, dx, ids, dwte, M, d, V,
+                     dropout);
   const long work = (long)T * (d / 4);
-  hipLaunchKernelGGL(embedding_bwd_pos_kernel, dim3((work + 255) / 256), dim3(256), 0, stream, dx, dwpe, B, T, d);
+  hipLaunchKernelGGL(embedding_bwd_pos_kernel, dim3((work + 255) / 256), dim3(256), 0, stream, dx, dwpe, B, T, d,
+                     dropout);
+  return hipGetLastError();
+}
+
+hipError_t launch_dropout_mask(DropoutArgs dropout, bool* out, long long n, hipStream_t stream) {
+  hipLaunchKernelGGL(dropout_mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dropout, out, n);
   return hipGetLastError();
 }
 

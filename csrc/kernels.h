@@ -12,6 +12,14 @@
 namespace llmt {
 
 // ---- LayerNorm --------------------------------------------------------------------------
+// Dropout site arguments (see common.h drop_keep): the site seed is already mixed with the step
+// seed on the host; thr = round(p * 65536), 0 disables the mask; scale = 1 / keep probability.
+struct DropoutArgs {
+  uint32_t seed = 0;
+  uint32_t thr = 0;
+  float scale = 1.f;
+};
+
 struct LnFwdArgs {
   const float* x;      // [M, d] residual stream
   const void* delta;   // [M, d] optional update added to x (bf16 or f32)
@@ -25,6 +33,7 @@ struct LnFwdArgs {
   float* rstd;         // [M]
   int M, d;
   float eps;
+  DropoutArgs dropout;  // applied to delta before the add (residual-branch dropout)
 };
 hipError_t launch_add_layernorm_fwd(const LnFwdArgs& a, hipStream_t stream);
 
@@ -43,6 +52,7 @@ struct LnBwdArgs {
   float* db;             // [d] accumulated
   float* dproj;          // optional [d] accumulated column sum of dx
   int M, d;
+  DropoutArgs dropout;   // mask of the branch that fed this stream: applied to dx_lp and dproj
 };
 hipError_t launch_layernorm_bwd(const LnBwdArgs& a, hipStream_t stream);
 
@@ -62,10 +72,13 @@ hipError_t launch_gelu_bwd(const void* dg, const void* u, void* du, float* dbias
 hipError_t launch_colsum_accum(const void* dy, bool bf16, float* out, int M, int N,
                                hipStream_t stream);
 // x[b*T+t] = wte[ids] + wpe[t]
+// x = dropout(wte[ids] + wpe[t]); the backward applies the same mask to dx before the scatter
 hipError_t launch_embedding_fwd(const int64_t* ids, const float* wte, const float* wpe, float* x,
-                                int B, int T, int d, int V, hipStream_t stream);
+                                int B, int T, int d, int V, DropoutArgs dropout, hipStream_t stream);
 hipError_t launch_embedding_bwd(const float* dx, const int64_t* ids, float* dwte, float* dwpe,
-                                int B, int T, int d, int V, hipStream_t stream);
+                                int B, int T, int d, int V, DropoutArgs dropout, hipStream_t stream);
+// keep-mask of elements 0..n-1 of one dropout site (tests)
+hipError_t launch_dropout_mask(DropoutArgs dropout, bool* out, long long n, hipStream_t stream);
 
 // ---- optimizer ---------------------------------------------------------------------------
 struct AdamWArgs {
@@ -94,13 +107,15 @@ hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, fl
 // ---- causal flash attention (head_dim 64) ----------------------------------------------
 // qkv [B, T, 3, H, 64] bf16 (the packed projection output), out [B, T, H, 64] bf16,
 // lse [B, H, T] f32 (natural-log normaliser).
+// `dropout` masks the attention probabilities (element (b, h, q, k) of the site: plane seed
+// mix32(seed + (b*H + h) * 0x9E3779B9), index q*T + k); lse stays the undropped normaliser
 hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H,
-                           hipStream_t stream);
+                           DropoutArgs dropout, hipStream_t stream);
 // dqkv [B, T, 3, H, 64] bf16; `delta` [B, H, T] f32 and `dq_part`
 // (attn_bwd_workspace_floats(B, T, H) floats) scratch
 long attn_bwd_workspace_floats(int B, int T, int H);
 hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse,
                            void* dqkv, float* delta, float* dq_part, int B, int T, int H,
-                           hipStream_t stream);
+                           DropoutArgs dropout, hipStream_t stream);
 
 }  // namespace llmt

@@ -48,7 +48,7 @@ template <int MAXC, typename TD, typename TY>
 __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
     const float* __restrict__ x, const TD* __restrict__ delta, const float* __restrict__ w,
     const float* __restrict__ b, float* __restrict__ xs_out, TY* __restrict__ y,
-    float* __restrict__ mean_out, float* __restrict__ rstd_out, int M, int d, float eps) {
+    float* __restrict__ mean_out, float* __restrict__ rstd_out, int M, int d, float eps, DropoutArgs dr) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * kLnWaves + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -62,7 +62,13 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
     if (c < nc) {
       v[j] = load4(xr + 4 * c);
       if (delta != nullptr) {
-        v[j] += load4(delta + row * d + 4 * c);
+        float4_t dv = load4(delta + row * d + 4 * c);
+        if (dr.thr != 0) {  // residual-branch dropout (reference gpt.py resid/mlp_dropout)
+          const uint64_t e0 = (uint64_t)row * d + 4 * c;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) dv[t] = drop_keep(dr.seed, dr.thr, e0 + t) ? dv[t] * dr.scale : 0.f;
+        }
+        v[j] += dv;
         store4(xs_out + row * d + 4 * c, v[j]);
       }
       s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
@@ -101,7 +107,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const TDY* __restrict__ dy, const float* __restrict__ xs, const float* __restrict__ mean,
     const float* __restrict__ rstd, const float* __restrict__ w, const float* __restrict__ dresid,
     const float* __restrict__ dy_scale, float* __restrict__ dx, TDY* __restrict__ dx_lp,
-    float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dproj, int M, int d) {
+    float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dproj, int M, int d, DropoutArgs dr) {
   extern __shared__ __attribute__((aligned(16))) float smem[];  // [kBwdWaves][3][d]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nc = d >> 2;
@@ -142,10 +148,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
         float4_t out = (g[j] * wv[j] - c1 - xh[j] * c2) * rs;
         if (dresid != nullptr) out += load4(dresid + row * d + 4 * c);
         store4(dx + row * d + 4 * c, out);
-        if (LOWP_OUT) store4(dx_lp + row * d + 4 * c, out);
+        // the branch that fed this residual stream sees its dropout mask (forward: add_ln_fwd)
+        float4_t br = out;
+        if (dr.thr != 0) {
+          const uint64_t e0 = (uint64_t)row * d + 4 * c;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) br[t] = drop_keep(dr.seed, dr.thr, e0 + t) ? out[t] * dr.scale : 0.f;
+        }
+        if (LOWP_OUT) store4(dx_lp + row * d + 4 * c, br);
         pw[j] += g[j] * xh[j];
         pb[j] += g[j];
-        pp[j] += out;
+        pp[j] += br;
       }
     }
   }
@@ -178,7 +191,7 @@ void launch_fwd_c(const LnFwdArgs& a, hipStream_t st) {
 #define LN_FWD(TD, TY)                                                                        \
   hipLaunchKernelGGL((add_ln_fwd_kernel<MAXC, TD, TY>), grid, block, 0, st, a.x,              \
                      (const TD*)a.delta, a.w, a.b, a.xs_out, (TY*)a.y, a.mean, a.rstd, a.M, a.d, \
-                     a.eps)
+                     a.eps, a.dropout)
   if (a.delta_bf16) {
     if (a.y_bf16) LN_FWD(bf16_raw, bf16_raw); else LN_FWD(bf16_raw, float);
   } else {
@@ -194,7 +207,7 @@ void launch_bwd_c(const LnBwdArgs& a, hipStream_t st) {
 #define LN_BWD(TDY, LP)                                                                         \
   hipLaunchKernelGGL((ln_bwd_kernel<MAXC, TDY, LP>), dim3(grid), dim3(256), shm, st,            \
                      (const TDY*)a.dy, a.xs, a.mean, a.rstd, a.w, a.dresid, a.dy_scale, a.dx,    \
-                     (TDY*)a.dx_lp, a.dw, a.db, a.dproj, a.M, a.d)
+                     (TDY*)a.dx_lp, a.dw, a.db, a.dproj, a.M, a.d, a.dropout)
   if (a.dy_bf16) {
     if (a.dx_lp != nullptr) LN_BWD(bf16_raw, true); else LN_BWD(bf16_raw, false);
   } else {

@@ -9,7 +9,7 @@ match the reference (``models/gpt.py:15-184``), so ``state_dict`` checkpoints ar
 Two execution paths share these parameters:
 
 * **module path** (``GPT.forward``) — ordinary autograd over PyTorch ops; used on CPU, for fp32
-  runs, for attention dropout > 0 and as the parity oracle in tests;
+  runs and as the parity oracle in tests;
 * **fused path** (``GPT.fused_loss``) — the hand-scheduled MI355X engine in
   :mod:`llmtrain.models.gpt_engine`: bf16 GEMMs on flat shadow weights, gfx950 HIP kernels for
   embedding / add+LayerNorm / flash attention / GELU / fused cross-entropy, a hand-written
@@ -165,10 +165,22 @@ class GPT(nn.Module):
 
     # -- fused path ------------------------------------------------------------------------
 
-    def fused_supported(self) -> bool:
-        """The fused engine implements dropout-free training (attention dropout would need an
-        in-kernel Philox stream; configs with ``dropout > 0`` use the module path)."""
-        return self.dropout == 0.0
+    def fused_supported(self, device_type: str = "cuda") -> bool:
+        """Whether the fused engine covers this shape on ``device_type``.  On the GPU the kernels
+        need head_dim 64 (the flash-attention specialisation, SURVEY §2.2 N1 — GPT-2 124M and XL
+        both use it) and LayerNorm widths d % 4 == 0, d <= 2048; other shapes train on the module
+        path.  On CPU the engine runs the reference ops, which take any shape.  Dropout is
+        supported everywhere (counter-based masks fused into the embedding, add+LayerNorm and
+        flash-attention kernels)."""
+        if device_type != "cuda":
+            return True
+        return (
+            self.d_model % self.n_heads == 0
+            and self.d_model // self.n_heads == 64
+            and self.d_model % 4 == 0
+            and self.d_model <= 2048
+            and self.d_ff % 8 == 0
+        )
 
     def prepare_runtime(self, *, compute_dtype: torch.dtype = torch.bfloat16) -> Any:
         """Move parameters into flat buffers and build the fused engine (idempotent).

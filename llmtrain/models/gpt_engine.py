@@ -14,6 +14,12 @@ forward (per block; ``M = B*T`` tokens, ``d`` model width, residual stream kept 
     g        = gelu(u)                            # HIP (exact erf GELU)
     delta    = g @ Wproj^T + b                    # hipBLASLt  (added by the next LN)
 
+Dropout (reference ``nn.Dropout`` after the embeddings, on the attention probabilities and on
+both residual branches, active in train mode) is fused into those kernels: each site's keep-mask
+is a counter-based hash of (step seed, site, element index) — see ``csrc/common.h`` — so the
+backward regenerates it instead of storing it.  Sites per forward: 0 = embedding, then per block
+``i``: ``1+3i`` attention-output branch, ``2+3i`` attention probabilities, ``3+3i`` MLP branch.
+
 then ``ln_f`` (+ the last residual add), the tied LM head GEMM against a vocab-padded bf16
 shadow (50257 → 50304 rows) and a fused softmax-cross-entropy kernel that produces the per-row
 loss AND overwrites the logits with their gradient in the same pass (the logits are dead after
@@ -43,6 +49,7 @@ from typing import Any
 import torch
 
 from llmtrain import ops
+from llmtrain.ops.reference import dropout_site_seed
 from llmtrain.runtime.flat import FlatParamStore
 
 __all__ = ["FusedGPTEngine"]
@@ -108,6 +115,14 @@ class _StepState:
     muf: torch.Tensor | None = None
     rsf: torch.Tensor | None = None
     dlogits: torch.Tensor | None = None
+    drop_p: float = 0.0
+    drop_seed: int = 0
+
+    def site(self, k: int) -> tuple[float, int]:
+        """``(p, site_seed)`` of dropout site ``k`` for this forward (``(0, 0)`` = off)."""
+        if self.drop_p <= 0.0:
+            return (0.0, 0)
+        return (self.drop_p, dropout_site_seed(self.drop_seed, k))
 
 
 class _FusedLoss(torch.autograd.Function):
@@ -209,6 +224,10 @@ class FusedGPTEngine:
         n_tok = bsz * seqlen
         cdt = self.compute_dtype
         state = _StepState(ids=ids, bsz=bsz, seqlen=seqlen)
+        if m.training and m.dropout > 0.0:
+            # one host draw per forward from torch's (seeded, checkpointed) CPU generator
+            state.drop_p = float(m.dropout)
+            state.drop_seed = int(torch.randint(0, 2**31 - 1, (1,)).item())
 
         if mask is not None:
             # The fused attention has no key-padding path: record padded batches on-device and
@@ -219,21 +238,28 @@ class FusedGPTEngine:
         else:
             row_w = torch.full((n_tok,), 1.0 / n_tok, dtype=torch.float32, device=ids.device)
 
-        x = ops.embedding_fwd(ids, m.token_embedding.weight, m.position_embedding.weight)
+        x = ops.embedding_fwd(ids, m.token_embedding.weight, m.position_embedding.weight, dropout=state.site(0))
         delta: torch.Tensor | None = None
-        for blk in self.blocks:
-            xs, h1, mu1, rs1 = ops.add_layernorm_fwd(x, delta, blk.ln_1.weight, blk.ln_1.bias, self.eps, cdt)
+        for i, blk in enumerate(self.blocks):
+            xs, h1, mu1, rs1 = ops.add_layernorm_fwd(
+                x, delta, blk.ln_1.weight, blk.ln_1.bias, self.eps, cdt, dropout=state.site(3 * i)
+            )  # site 3i = the previous block's MLP branch (unused for block 0: delta is None)
             qkv = self._linear(h1, blk.attn.qkv_proj)
-            att, lse = ops.attn_fwd(qkv, bsz, seqlen, self.n_heads)
+            att, lse = ops.attn_fwd(qkv, bsz, seqlen, self.n_heads, dropout=state.site(2 + 3 * i))
             y = self._linear(att, blk.attn.out_proj)
-            xm, h2, mu2, rs2 = ops.add_layernorm_fwd(xs, y, blk.ln_2.weight, blk.ln_2.bias, self.eps, cdt)
+            xm, h2, mu2, rs2 = ops.add_layernorm_fwd(
+                xs, y, blk.ln_2.weight, blk.ln_2.bias, self.eps, cdt, dropout=state.site(1 + 3 * i)
+            )
             u = self._linear(h2, blk.mlp_fc)
             g = ops.gelu_fwd(u)
             delta = self._linear(g, blk.mlp_proj)
             x = xm
             if keep:
                 state.blocks.append(_BlockActs(xs, h1, mu1, rs1, qkv, att, lse, xm, h2, mu2, rs2, u, g))
-        xf, hf, muf, rsf = ops.add_layernorm_fwd(x, delta, m.ln_f.weight, m.ln_f.bias, self.eps, cdt)
+        n_layers = len(self.blocks)
+        xf, hf, muf, rsf = ops.add_layernorm_fwd(
+            x, delta, m.ln_f.weight, m.ln_f.bias, self.eps, cdt, dropout=state.site(3 * n_layers)
+        )
         head = self.store.shadow_of(self.head_weight, padded=True)
         logits = torch.mm(hf, head.t())  # [M, Vp]
         per_row = ops.cross_entropy_fwd_bwd(logits, labels.reshape(-1), self.vocab, row_w)
@@ -266,9 +292,10 @@ class FusedGPTEngine:
         del dlogits
 
         last = self.blocks[-1]
+        n_layers = len(self.blocks)
         dx, dx_lp = ops.layernorm_bwd(
             dhf, st.xf, st.muf, st.rsf, m.ln_f.weight, None, self._g(m.ln_f.weight), self._g(m.ln_f.bias),
-            go, want_lowp=True, dproj_bias=self._g(last.mlp_proj.bias),
+            go, want_lowp=True, dproj_bias=self._g(last.mlp_proj.bias), dropout=st.site(3 * n_layers),
         )
         del dhf
         self._notify("ln_f")
@@ -285,14 +312,14 @@ class FusedGPTEngine:
             del du
             dxm, dy_lp = ops.layernorm_bwd(
                 dh2, a.xm, a.mu2, a.rs2, blk.ln_2.weight, dx, self._g(blk.ln_2.weight), self._g(blk.ln_2.bias),
-                None, want_lowp=True, dproj_bias=self._g(blk.attn.out_proj.bias),
+                None, want_lowp=True, dproj_bias=self._g(blk.attn.out_proj.bias), dropout=st.site(1 + 3 * i),
             )
             del dh2, dx, dx_lp
             # attention output projection
             self._wgrad(self._g(blk.attn.out_proj.weight), dy_lp, a.att)
             datt = torch.mm(dy_lp, self._w(blk.attn.out_proj.weight))
             del dy_lp
-            dqkv = ops.attn_bwd(datt, a.qkv, a.att, a.lse, bsz, seqlen, self.n_heads)
+            dqkv = ops.attn_bwd(datt, a.qkv, a.att, a.lse, bsz, seqlen, self.n_heads, dropout=st.site(2 + 3 * i))
             del datt
             ops.colsum_accum(dqkv, self._g(blk.attn.qkv_proj.bias))
             self._wgrad(self._g(blk.attn.qkv_proj.weight), dqkv, a.h1)
@@ -301,11 +328,13 @@ class FusedGPTEngine:
             prev_bias = self._g(self.blocks[i - 1].mlp_proj.bias) if i > 0 else None
             dx, dx_lp = ops.layernorm_bwd(
                 dh1, a.xs, a.mu1, a.rs1, blk.ln_1.weight, dxm, self._g(blk.ln_1.weight), self._g(blk.ln_1.bias),
-                None, want_lowp=i > 0, dproj_bias=prev_bias,
+                None, want_lowp=i > 0, dproj_bias=prev_bias, dropout=st.site(3 * i) if i > 0 else (0.0, 0),
             )
             del dh1, dxm
             st.blocks[i] = None  # type: ignore[call-overload]  # free activations early
             self._notify(f"block{i}")
 
-        ops.embedding_bwd(dx, st.ids, self._g(m.token_embedding.weight), self._g(m.position_embedding.weight))
+        ops.embedding_bwd(
+            dx, st.ids, self._g(m.token_embedding.weight), self._g(m.position_embedding.weight), dropout=st.site(0)
+        )
         self._notify("embed")

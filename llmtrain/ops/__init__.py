@@ -39,33 +39,39 @@ def _on_gpu(t: torch.Tensor) -> bool:
     return t.device.type == "cuda"
 
 
-def add_layernorm_fwd(x, delta, weight, bias, eps: float, out_dtype: torch.dtype):
+def add_layernorm_fwd(x, delta, weight, bias, eps: float, out_dtype: torch.dtype, dropout=(0.0, 0)):
+    """``xs = x + dropout(delta)``, ``y = LN(xs)``; ``dropout = (p, site_seed)`` masks the branch."""
+    p, seed = dropout
     if _on_gpu(x):
-        xs, y, mean, rstd = hip_ops().add_layernorm_fwd(x, delta, weight, bias, eps, out_dtype)
+        xs, y, mean, rstd = hip_ops().add_layernorm_fwd(x, delta, weight, bias, eps, out_dtype, p, seed)
         return (x if delta is None else xs), y, mean, rstd
-    return ref.add_layernorm_fwd(x, delta, weight, bias, eps, out_dtype)
+    return ref.add_layernorm_fwd(x, delta, weight, bias, eps, out_dtype, p, seed)
 
 
 def layernorm_bwd(
-    dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale=None, *, want_lowp=False, dproj_bias=None
+    dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale=None, *, want_lowp=False, dproj_bias=None,
+    dropout=(0.0, 0),
 ):
     """LayerNorm backward with two optional fusions for the producer of the normalised input:
 
     * ``want_lowp`` also returns ``dx`` in ``dy``'s dtype (the GEMM operand of the projection
       whose output was added to the residual stream), and
-    * ``dproj_bias`` (fp32 ``[d]``) accumulates ``colsum(dx)`` — that projection's bias grad.
+    * ``dproj_bias`` (fp32 ``[d]``) accumulates ``colsum(dx)`` — that projection's bias grad;
 
-    Returns ``(dx_fp32, dx_lowp | None)``.
+    both see the branch's dropout mask ``dropout = (p, site_seed)`` (the fp32 ``dx`` of the
+    residual stream itself does not).  Returns ``(dx_fp32, dx_lowp | None)``.
     """
+    p, seed = dropout
     if _on_gpu(dy):
         dx, dx_lp = hip_ops().layernorm_bwd(
-            dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale, want_lowp, dproj_bias
+            dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale, want_lowp, dproj_bias, p, seed
         )
         return dx, (dx_lp if want_lowp else None)
     dx = ref.layernorm_bwd(dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale)
+    branch = ref._apply_dropout(dx, p, seed)
     if dproj_bias is not None:
-        ref.colsum_accum(dx, dproj_bias)
-    return dx, (dx.to(dy.dtype) if want_lowp else None)
+        ref.colsum_accum(branch, dproj_bias)
+    return dx, (branch.to(dy.dtype) if want_lowp else None)
 
 
 def cross_entropy_fwd_bwd(logits, labels, vocab: int, row_weight):
@@ -93,29 +99,33 @@ def colsum_accum(dy, out) -> None:
         ref.colsum_accum(dy, out)
 
 
-def embedding_fwd(ids, wte, wpe):
+def embedding_fwd(ids, wte, wpe, dropout=(0.0, 0)):
+    p, seed = dropout
     if _on_gpu(ids):
-        return hip_ops().embedding_fwd(ids, wte, wpe)
-    return ref.embedding_fwd(ids, wte, wpe)
+        return hip_ops().embedding_fwd(ids, wte, wpe, p, seed)
+    return ref.embedding_fwd(ids, wte, wpe, p, seed)
 
 
-def embedding_bwd(dx, ids, dwte, dwpe) -> None:
+def embedding_bwd(dx, ids, dwte, dwpe, dropout=(0.0, 0)) -> None:
+    p, seed = dropout
     if _on_gpu(dx):
-        hip_ops().embedding_bwd(dx, ids, dwte, dwpe)
+        hip_ops().embedding_bwd(dx, ids, dwte, dwpe, p, seed)
     else:
-        ref.embedding_bwd(dx, ids, dwte, dwpe)
+        ref.embedding_bwd(dx, ids, dwte, dwpe, p, seed)
 
 
-def attn_fwd(qkv, bsz: int, seqlen: int, n_heads: int):
+def attn_fwd(qkv, bsz: int, seqlen: int, n_heads: int, dropout=(0.0, 0)):
+    p, seed = dropout
     if _on_gpu(qkv):
-        return hip_ops().attn_fwd(qkv, bsz, seqlen, n_heads)
-    return ref.attn_fwd(qkv, bsz, seqlen, n_heads)
+        return hip_ops().attn_fwd(qkv, bsz, seqlen, n_heads, p, seed)
+    return ref.attn_fwd(qkv, bsz, seqlen, n_heads, p, seed)
 
 
-def attn_bwd(dout, qkv, out, lse, bsz: int, seqlen: int, n_heads: int):
+def attn_bwd(dout, qkv, out, lse, bsz: int, seqlen: int, n_heads: int, dropout=(0.0, 0)):
+    p, seed = dropout
     if _on_gpu(dout):
-        return hip_ops().attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads)
-    return ref.attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads)
+        return hip_ops().attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads, p, seed)
+    return ref.attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads, p, seed)
 
 
 def wgrad_accum(dst, dy, x) -> None:

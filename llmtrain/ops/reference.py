@@ -21,6 +21,9 @@ import torch.nn.functional as F
 
 __all__ = [
     "adamw_flat",
+    "dropout_keep",
+    "dropout_params",
+    "dropout_site_seed",
     "add_layernorm_fwd",
     "attn_bwd",
     "attn_fwd",
@@ -36,6 +39,71 @@ __all__ = [
 
 _INV_SQRT2 = 1.0 / math.sqrt(2.0)
 _INV_SQRT_2PI = 1.0 / math.sqrt(2.0 * math.pi)
+_M32 = 0xFFFFFFFF
+
+
+# ---- dropout masks (bit-identical to csrc/common.h drop_keep) --------------------------------
+
+
+def _mix32(x: torch.Tensor) -> torch.Tensor:
+    """lowbias32 on int64 tensors holding uint32 values (products wrap mod 2^64; low 32 bits exact)."""
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
+
+
+def mix32_int(x: int) -> int:
+    """Scalar lowbias32 (host-side seed derivation)."""
+    x &= _M32
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & _M32
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
+
+
+def dropout_site_seed(step_seed: int, site: int) -> int:
+    """Seed of one dropout site (one tensor of one layer) for one forward pass."""
+    return mix32_int((step_seed & _M32) ^ ((site * 0x9E3779B9) & _M32))
+
+
+def dropout_params(p: float) -> tuple[int, float]:
+    """``(thr, scale)`` exactly as the HIP side derives them (thr = round(p * 2^16))."""
+    thr = min(int(round(p * 65536.0)), 65535) if p > 0 else 0
+    return thr, (65536.0 / (65536 - thr) if thr else 1.0)
+
+
+def dropout_keep(seed: int, thr: int, idx: torch.Tensor) -> torch.Tensor:
+    """Keep-mask for element indices ``idx`` (int64) of a site with ``seed``."""
+    if thr == 0:
+        return torch.ones_like(idx, dtype=torch.bool)
+    pair = idx >> 1
+    h = _mix32((pair & _M32) ^ (seed & _M32) ^ (((pair >> 32) * 0x85EBCA6B) & _M32))
+    half = torch.where((idx & 1).bool(), h >> 16, h & 0xFFFF)
+    return half >= thr
+
+
+def _apply_dropout(x: torch.Tensor, p: float, seed: int) -> torch.Tensor:
+    """Mask a row-major tensor whose element ``i`` (flat index) belongs to the site."""
+    thr, scale = dropout_params(p)
+    if thr == 0:
+        return x
+    idx = torch.arange(x.numel(), device=x.device, dtype=torch.int64).view(x.shape)
+    return torch.where(dropout_keep(seed, thr, idx), x * scale, torch.zeros_like(x))
+
+
+def attn_dropout_keep(seed: int, p: float, bsz: int, n_heads: int, seqlen: int, device) -> torch.Tensor:
+    """``[B, H, T, T]`` keep-mask of attention probabilities (plane seed per (b, h), index q*T+k)."""
+    thr, _ = dropout_params(p)
+    bh = torch.arange(bsz * n_heads, dtype=torch.int64, device=device)
+    pseed = _mix32((seed + bh * 0x9E3779B9) & _M32).view(bsz, n_heads, 1, 1)
+    e = torch.arange(seqlen * seqlen, dtype=torch.int64, device=device).view(1, 1, seqlen, seqlen)
+    pair = e >> 1
+    h = _mix32((pair ^ pseed) & _M32)
+    half = torch.where((e & 1).bool(), h >> 16, h & 0xFFFF)
+    return half >= thr
 
 
 def add_layernorm_fwd(
@@ -45,12 +113,14 @@ def add_layernorm_fwd(
     bias: torch.Tensor,
     eps: float,
     out_dtype: torch.dtype,
+    dropout_p: float = 0.0,
+    dropout_seed: int = 0,
 ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
-    """``xs = x + delta`` (fp32 residual update), ``y = LN(xs)`` cast to ``out_dtype``.
+    """``xs = x + dropout(delta)`` (fp32 residual update), ``y = LN(xs)`` cast to ``out_dtype``.
 
     Returns ``(xs, y, mean, rstd)``; when ``delta`` is None ``xs`` is ``x`` itself.
     """
-    xs = x if delta is None else x + delta.float()
+    xs = x if delta is None else x + _apply_dropout(delta.float(), dropout_p, dropout_seed)
     mean = xs.mean(dim=-1)
     var = (xs - mean[:, None]).pow(2).mean(dim=-1)
     rstd = torch.rsqrt(var + eps)
@@ -133,18 +203,26 @@ def colsum_accum(dy: torch.Tensor, out: torch.Tensor) -> None:
     out += dy.float().sum(dim=0)
 
 
-def embedding_fwd(ids: torch.Tensor, wte: torch.Tensor, wpe: torch.Tensor) -> torch.Tensor:
-    """``x[b*T+t] = wte[ids[b,t]] + wpe[t]`` → ``[B*T, d]`` fp32."""
+def embedding_fwd(
+    ids: torch.Tensor, wte: torch.Tensor, wpe: torch.Tensor, dropout_p: float = 0.0, dropout_seed: int = 0
+) -> torch.Tensor:
+    """``x[b*T+t] = dropout(wte[ids[b,t]] + wpe[t])`` → ``[B*T, d]`` fp32."""
     bsz, seqlen = ids.shape
     x = wte.float()[ids.reshape(-1)] + wpe.float()[:seqlen].repeat(bsz, 1)
-    return x
+    return _apply_dropout(x, dropout_p, dropout_seed)
 
 
 def embedding_bwd(
-    dx: torch.Tensor, ids: torch.Tensor, dwte: torch.Tensor, dwpe: torch.Tensor
+    dx: torch.Tensor,
+    ids: torch.Tensor,
+    dwte: torch.Tensor,
+    dwpe: torch.Tensor,
+    dropout_p: float = 0.0,
+    dropout_seed: int = 0,
 ) -> None:
-    """Scatter-add token gradients into ``dwte``; sum over the batch into ``dwpe[:T]``."""
+    """Scatter-add (masked) token gradients into ``dwte``; sum over the batch into ``dwpe[:T]``."""
     bsz, seqlen = ids.shape
+    dx = _apply_dropout(dx.float(), dropout_p, dropout_seed)
     dwte.index_add_(0, ids.reshape(-1), dx.float())
     dwpe[:seqlen] += dx.float().view(bsz, seqlen, -1).sum(dim=0)
 
@@ -155,10 +233,12 @@ def _split_qkv(qkv: torch.Tensor, bsz: int, seqlen: int, n_heads: int):
     return q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
 
 
-def attn_fwd(qkv: torch.Tensor, bsz: int, seqlen: int, n_heads: int) -> tuple[torch.Tensor, torch.Tensor]:
-    """Causal attention over packed ``qkv`` ``[B*T, 3d]``.
+def attn_fwd(
+    qkv: torch.Tensor, bsz: int, seqlen: int, n_heads: int, dropout_p: float = 0.0, dropout_seed: int = 0
+) -> tuple[torch.Tensor, torch.Tensor]:
+    """Causal attention over packed ``qkv`` ``[B*T, 3d]`` with optional probability dropout.
 
-    Returns ``out`` ``[B*T, d]`` (dtype of qkv) and ``lse`` ``[B, H, T]`` fp32.
+    Returns ``out`` ``[B*T, d]`` (dtype of qkv) and ``lse`` ``[B, H, T]`` fp32 (undropped).
     """
     q, k, v = (t.float() for t in _split_qkv(qkv, bsz, seqlen, n_heads))
     hd = q.shape[-1]
@@ -167,6 +247,10 @@ def attn_fwd(qkv: torch.Tensor, bsz: int, seqlen: int, n_heads: int) -> tuple[to
     s = s.masked_fill(causal, float("-inf"))
     lse = torch.logsumexp(s, dim=-1)
     p = torch.exp(s - lse[..., None])
+    thr, dscale = dropout_params(dropout_p)
+    if thr:
+        keep = attn_dropout_keep(dropout_seed, dropout_p, bsz, n_heads, seqlen, qkv.device)
+        p = torch.where(keep, p * dscale, torch.zeros_like(p))
     out = (p @ v).transpose(1, 2).reshape(bsz * seqlen, n_heads * hd)
     return out.to(qkv.dtype), lse
 
@@ -179,6 +263,8 @@ def attn_bwd(
     bsz: int,
     seqlen: int,
     n_heads: int,
+    dropout_p: float = 0.0,
+    dropout_seed: int = 0,
 ) -> torch.Tensor:
     """Gradient of :func:`attn_fwd` w.r.t. packed ``qkv``; returns ``[B*T, 3d]`` in qkv dtype."""
     q, k, v = (t.float() for t in _split_qkv(qkv, bsz, seqlen, n_heads))
@@ -189,8 +275,13 @@ def attn_bwd(
     s = (q @ k.transpose(-2, -1)) * scale
     causal = torch.ones(seqlen, seqlen, dtype=torch.bool, device=qkv.device).triu(1)
     p = torch.exp(s - lse[..., None]).masked_fill(causal, 0.0)
-    dv = p.transpose(-2, -1) @ do
+    thr, dscale = dropout_params(dropout_p)
+    keep = attn_dropout_keep(dropout_seed, dropout_p, bsz, n_heads, seqlen, qkv.device) if thr else None
+    pd = p if keep is None else torch.where(keep, p * dscale, torch.zeros_like(p))
+    dv = pd.transpose(-2, -1) @ do
     dp = do @ v.transpose(-2, -1)
+    if keep is not None:
+        dp = torch.where(keep, dp * dscale, torch.zeros_like(dp))
     delta = (do * o).sum(dim=-1, keepdim=True)
     ds = p * (dp - delta) * scale
     dq = ds @ k

@@ -24,6 +24,7 @@ What changes on the MI355X path:
 from __future__ import annotations
 
 import contextlib
+import dataclasses
 import logging
 import math
 import time
@@ -140,10 +141,14 @@ class Trainer:
         self._val_loader = data_module.val_dataloader()
 
         local_rank = ddp_state.local_rank if ddp_state is not None else 0
-        fused_capable = hasattr(model, "prepare_runtime") and bool(
-            getattr(model, "fused_supported", lambda: False)()
-        )
-        self._policy = resolve_policy(cfg, local_rank=local_rank, fused_capable=fused_capable)
+        supported = getattr(model, "fused_supported", None)
+        fused_capable = hasattr(model, "prepare_runtime") and supported is not None
+        policy = resolve_policy(cfg, local_rank=local_rank, fused_capable=fused_capable)
+        if policy.use_fused and not supported(policy.device.type):
+            logger.warning("trainer: fused engine does not cover this model shape on %s; using the module path",
+                           policy.device)
+            policy = dataclasses.replace(policy, use_fused=False)
+        self._policy = policy
         self._device = self._policy.device
         model = model.to(self._device)
         if self._policy.use_fused:

@@ -19,7 +19,7 @@ import torch.distributed as dist
 
 from llmtrain.config.schemas import RunConfig
 
-__all__ = ["DDPState", "resolve_backend", "setup_ddp", "teardown_ddp"]
+__all__ = ["DDPState", "ReplicaMismatchError", "resolve_backend", "setup_ddp", "teardown_ddp", "verify_replicas"]
 
 logger = logging.getLogger(__name__)
 
@@ -114,3 +114,36 @@ def teardown_ddp() -> None:
     if dist.is_initialized():
         logger.info("Destroying DDP process group")
         dist.destroy_process_group()
+
+
+class ReplicaMismatchError(RuntimeError):
+    """Data-parallel ranks hold different parameters (SURVEY §5.2 consistency check)."""
+
+
+def verify_replicas(params, *, device, tag: str, rtol: float = 0.0) -> tuple[float, float]:  # type: ignore[no-untyped-def]
+    """Compare a parameter checksum across ranks: ``(Σ p, Σ p²)`` in fp64 on every rank,
+    all-reduced with MAX and MIN (two tiny collectives).  Raises :class:`ReplicaMismatchError` when
+    any rank differs by more than ``rtol`` (0 = bitwise-equal sums, which identical replicas always
+    produce because every rank reduces the same values in the same order).  Called after the
+    data-parallel wrap (rank-0 broadcast) and after a resume."""
+    import torch
+
+    parts = []
+    with torch.no_grad():
+        for p in params:
+            v = p.detach().to(torch.float64)
+            parts.append(torch.stack([v.sum(), (v * v).sum()]))
+    total = torch.stack(parts).sum(dim=0).to(device) if parts else torch.zeros(2, dtype=torch.float64, device=device)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(total[0]), float(total[1])
+    hi, lo = total.clone(), total.clone()
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    spread = (hi - lo).abs()
+    limit = rtol * hi.abs().clamp_min(1.0)
+    if bool((spread > limit).any()):
+        raise ReplicaMismatchError(
+            f"{tag}: parameter checksums differ across ranks (sum spread {float(spread[0]):.3e}, "
+            f"sumsq spread {float(spread[1]):.3e})"
+        )
+    return float(total[0]), float(total[1])

@@ -38,6 +38,7 @@ from torch import nn
 
 from llmtrain.config.schemas import RunConfig
 from llmtrain.parallel.ddp import unwrap, wrap_data_parallel
+from llmtrain.parallel.dist import verify_replicas
 from llmtrain.parallel.dist import DDPState
 from llmtrain.registry import initialize_registries
 from llmtrain.registry.data import get_data_module
@@ -156,6 +157,7 @@ class Trainer:
         self._model: nn.Module = model
         if self._is_ddp_active:
             self._model = wrap_data_parallel(model, cfg, self._device)
+            verify_replicas(model.parameters(), device=self._metric_device(), tag="after data-parallel wrap")
 
         self._optimizer = build_optimizer(unwrap(self._model), cfg.trainer.lr, cfg.trainer.weight_decay)
         self._scheduler = self._build_scheduler(self._optimizer)
@@ -388,6 +390,8 @@ class Trainer:
             if payload["config"] != self._cfg.model_dump():
                 logger.warning("checkpoint: config mismatch detected; using current config for resume")
             resumed_from_step = self.restore(payload)
+            if self._is_ddp_active:
+                verify_replicas(self._raw_model.parameters(), device=self._metric_device(), tag="after resume")
             start_step = resumed_from_step + 1
             if start_step > max_steps:
                 logger.info(

@@ -106,6 +106,21 @@ def _reducer_worker(rank: int, world: int, port: int, out_dir: str) -> None:
     model.prepare_runtime(compute_dtype=torch.float32)
     ddp = FlatDataParallel(model, bucket_cap_mb=0.01)
     assert len(ddp.buckets) > 2
+    from llmtrain.parallel.dist import ReplicaMismatchError, verify_replicas
+
+    verify_replicas(model.parameters(), device=torch.device("cpu"), tag="test")  # broadcast made them equal
+    if rank == 1:
+        with torch.no_grad():
+            model.flat_store.master[0] += 1.0  # diverge one rank ...
+    try:
+        verify_replicas(model.parameters(), device=torch.device("cpu"), tag="diverged")
+        raise AssertionError("mismatch not detected")
+    except ReplicaMismatchError:
+        pass  # ... and every rank sees it
+    if rank == 1:
+        with torch.no_grad():
+            model.flat_store.master[0] -= 1.0
+    verify_replicas(model.parameters(), device=torch.device("cpu"), tag="restored")
     g = torch.Generator().manual_seed(99 + rank)
     batches = [torch.randint(0, 50, (2, 8), generator=g) for _ in range(2)]
     model.flat_store.zero_grad()

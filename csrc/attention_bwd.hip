@@ -33,15 +33,24 @@ constexpr int kBwdWaves = 8;
 constexpr int kKvBlk = 32 * kBwdWaves;  // 256 keys per workgroup
 constexpr int kQTile = 64;  // query rows per sweep step (two 32-row MFMA tiles)
 
-// delta[b, h, t] = sum_d dO[b, t, h, d] * O[b, t, h, d]; 8 lanes per row
+// delta[b, h, t] = sum_d dO[b, t, h, d] * O[b, t, h, d]; a workgroup owns 32 consecutive t of one
+// (b, h), 8 lanes per row.  With `dbias_v` it also accumulates the column sums of dO per head:
+// without dropout every valid row of P sums to 1, so sum_key dV[key, d] = sum_q dO[q, d] — the
+// V part of the qkv-bias gradient costs one LDS reduction here instead of a pass over dqkv.
 __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restrict__ dout,
                                                          const bf16_raw* __restrict__ out,
-                                                         float* __restrict__ delta, int T, int H, long rows) {
-  const long row = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 3;  // row = (b*T + t)*H + h
-  const int sub = threadIdx.x & 7;
+                                                         float* __restrict__ delta, float* __restrict__ dbias_v,
+                                                         int T, int H) {
+  __shared__ float red[32][65];
+  const int bh = blockIdx.y;
+  const int b = bh / H, h = bh - b * H;
+  const int rl = threadIdx.x >> 3, sub = threadIdx.x & 7;
+  const int t = blockIdx.x * 32 + rl;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float acc = 0.f;
-  if (row < rows) {
-    float a[8], o[8];
+  if (t < T) {
+    const long row = ((long)b * T + t) * H + h;
+    float o[8];
     unpack8(*reinterpret_cast<const ushort8_t*>(dout + row * kHD + 8 * sub), a);
     unpack8(*reinterpret_cast<const ushort8_t*>(out + row * kHD + 8 * sub), o);
 #pragma unroll
@@ -50,11 +59,15 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
   acc += __shfl_xor(acc, 1, 64);
   acc += __shfl_xor(acc, 2, 64);
   acc += __shfl_xor(acc, 4, 64);
-  if (row < rows && sub == 0) {
-    const long bt = row / H;
-    const int h = (int)(row - bt * H);
-    const long b = bt / T, t = bt - b * T;
-    delta[(b * H + h) * T + t] = acc;
+  if (t < T && sub == 0) delta[(long)bh * T + t] = acc;
+  if (dbias_v == nullptr) return;  // uniform: kernel argument
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[rl][8 * sub + i] = a[i];
+  __syncthreads();
+  if (threadIdx.x < kHD) {
+    float s = 0.f;
+    for (int r = 0; r < 32; ++r) s += red[r][threadIdx.x];
+    atomicAdd(dbias_v + h * kHD + threadIdx.x, s);
   }
 }
 
@@ -62,28 +75,49 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
 // the main kernel stores each key block's dQ contribution with plain stores (no memset, no
 // atomics); rows only ever read the partials their causal key blocks wrote.
 __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const float* __restrict__ part, bf16_raw* __restrict__ dqkv,
-                                                             int T, int H, int nkb, long n8) {
+                                                             float* __restrict__ dbias, int T, int H, int nkb, long n8) {
+  __shared__ float red[32][65];  // [row in block][d] for the Q-bias column sums
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // one 8-element chunk
-  if (i >= n8) return;
   const long row = i >> 3;  // (b*H + h)*T + t
   const int c = (int)(i & 7);
   const long bh = row / T;
   const int t = (int)(row - bh * T);
   const long b = bh / H;
   const int h = (int)(bh - b * H);
-  const long plane = n8 * 8;  // floats per key-block partial
-  const int last = min(t / kKvBlk, nkb - 1);
   float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int kb = 0; kb <= last; ++kb) {
-    const float4_t* src = reinterpret_cast<const float4_t*>(part + kb * plane + row * kHD + 8 * c);
-    const float4_t x = src[0], y = src[1];
+  if (i < n8) {
+    const long plane = n8 * 8;  // floats per key-block partial
+    const int last = min(t / kKvBlk, nkb - 1);
+    for (int kb = 0; kb <= last; ++kb) {
+      const float4_t* src = reinterpret_cast<const float4_t*>(part + kb * plane + row * kHD + 8 * c);
+      const float4_t x = src[0], y = src[1];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      f[j] += x[j];
-      f[4 + j] += y[j];
+      for (int j = 0; j < 4; ++j) {
+        f[j] += x[j];
+        f[4 + j] += y[j];
+      }
     }
+    *reinterpret_cast<ushort8_t*>(dqkv + ((b * T + t) * 3L * H + h) * kHD + 8 * c) = pack8(f);
   }
-  *reinterpret_cast<ushort8_t*>(dqkv + ((b * T + t) * 3L * H + h) * kHD + 8 * c) = pack8(f);
+  if (dbias == nullptr) return;  // uniform: kernel argument
+  // Q part of the qkv-bias gradient: sum this block's 32 rows per head column
+  const long row0 = ((long)blockIdx.x * blockDim.x) >> 3;
+  const long last_row = min(row0 + 31, n8 / 8 - 1);
+  if (row0 / T == last_row / T) {  // the block's rows share one (b, h): LDS reduction, 64 atomics
+    const int rl = threadIdx.x >> 3;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[rl][8 * c + j] = f[j];
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      float acc = 0.f;
+      for (int r = 0; r < 32; ++r) acc += red[r][threadIdx.x];
+      const int hh = (int)((row0 / T) % H);
+      atomicAdd(dbias + hh * kHD + threadIdx.x, acc);
+    }
+  } else if (i < n8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(dbias + h * kHD + 8 * c + j, f[j]);
+  }
 }
 
 // raw 16-byte / 4-byte buffer loads: offsets past the descriptor's record count read as zero
@@ -106,12 +140,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta,
                                                           bf16_raw* __restrict__ dqkv,
-                                                          float* __restrict__ dq_part, int T, int H, int nkb,
-                                                          DropoutArgs dr) {
+                                                          float* __restrict__ dq_part, float* __restrict__ dbias,
+                                                          int T, int H, int nkb, DropoutArgs dr) {
   __shared__ __attribute__((aligned(16))) bf16_raw kt_lds[kHD * kKvBlk];             // K^T, 32 KB
   __shared__ __attribute__((aligned(16))) bf16_raw qd_lds[2][2][kQTile * kHD];      // [buf][Q|dO] 32 KB
   __shared__ __attribute__((aligned(16))) bf16_raw ds_lds[2][kKvBlk * kQTile];      // [buf][key][q] 64 KB
   __shared__ __attribute__((aligned(16))) float rowc_lds[2][2 * kQTile];            // lse*log2e | delta
+  __shared__ float bias_red[kBwdWaves][kHD];                                       // V bias (dropout)
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -352,6 +387,28 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
       }
     }
   }
+  // qkv-bias gradient, K and V parts.  K: exactly zero — adding b_k shifts every score of a query
+  // row by q.b_k, which softmax ignores — so nothing is accumulated.  V without dropout: the
+  // delta kernel's column sums of dO.  V with dropout (rows of the dropped P no longer sum to 1):
+  // sum this block's 256 keys of dV^T — over the 32 lanes of each half, then over the 8 waves.
+  if (!DROPOUT || dbias == nullptr) return;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float vv = dv[dt][r];
+#pragma unroll
+      for (int off = 1; off < 32; off <<= 1) vv += __shfl_xor(vv, off, 64);
+      if (col == 0) bias_red[wave][dt * 32 + 8 * (r >> 2) + 4 * half + (r & 3)] = vv;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < kHD) {
+    float acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < kBwdWaves; ++w) acc += bias_red[w][threadIdx.x];
+    atomicAdd(dbias + (2 * H + h) * kHD + threadIdx.x, acc);
+  }
 }
 
 }  // namespace attn
@@ -362,22 +419,25 @@ long attn_bwd_workspace_floats(int B, int T, int H) {
 }
 
 hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse, void* dqkv,
-                           float* delta, float* dq_part, int B, int T, int H, DropoutArgs dropout,
-                           hipStream_t stream) {
+                           float* delta, float* dq_part, float* dbias, int B, int T, int H,
+                           DropoutArgs dropout, hipStream_t stream) {
   if (B <= 0 || T <= 0 || H <= 0 || T > 65535) return hipErrorInvalidValue;
   const long rows = (long)B * T * H;
-  hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, stream,
-                     (const bf16_raw*)dout, (const bf16_raw*)out, delta, T, H, rows);
+  hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((T + 31) / 32, B * H), dim3(256), 0, stream,
+                     (const bf16_raw*)dout, (const bf16_raw*)out, delta,
+                     dropout.thr == 0 && dbias != nullptr ? dbias + 2L * H * attn::kHD : nullptr, T, H);
   const int nkb = (T + attn::kKvBlk - 1) / attn::kKvBlk;
   if (dropout.thr != 0)
     hipLaunchKernelGGL(attn::attn_bwd_kernel<true>, dim3(B * H, nkb), dim3(512), 0, stream, (const bf16_raw*)qkv,
-                       (const bf16_raw*)dout, lse, delta, (bf16_raw*)dqkv, dq_part, T, H, nkb, dropout);
+                       (const bf16_raw*)dout, lse, delta, (bf16_raw*)dqkv, dq_part, dbias, T, H, nkb,
+                       dropout);
   else
     hipLaunchKernelGGL(attn::attn_bwd_kernel<false>, dim3(B * H, nkb), dim3(512), 0, stream, (const bf16_raw*)qkv,
-                       (const bf16_raw*)dout, lse, delta, (bf16_raw*)dqkv, dq_part, T, H, nkb, dropout);
+                       (const bf16_raw*)dout, lse, delta, (bf16_raw*)dqkv, dq_part, dbias, T, H, nkb,
+                       dropout);
   const long n8 = rows * attn::kHD / 8;
   hipLaunchKernelGGL(attn::attn_dq_reduce_kernel, dim3((n8 + 255) / 256), dim3(256), 0, stream, dq_part,
-                     (bf16_raw*)dqkv, T, H, nkb, n8);
+                     (bf16_raw*)dqkv, dbias, T, H, nkb, n8);
   return hipGetLastError();
 }
 

@@ -286,7 +286,7 @@ std::tuple<Tensor, Tensor> attn_fwd(const Tensor& qkv, int64_t B, int64_t T, int
 }
 
 Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const Tensor& lse, int64_t B, int64_t T,
-                int64_t H, double dropout_p, int64_t dropout_seed) {
+                int64_t H, double dropout_p, int64_t dropout_seed, const c10::optional<Tensor>& dbias) {
   check_qkv(qkv, B, T, H);
   for (const Tensor* t : {&dout, &out}) {
     check_gpu(*t, "dout/out");
@@ -300,8 +300,15 @@ Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const 
   Tensor dqkv = at::empty_like(qkv);
   Tensor delta = at::empty({B, H, T}, lse.options());
   Tensor dq = at::empty({llmt::attn_bwd_workspace_floats((int)B, (int)T, (int)H)}, lse.options());
+  float* db = nullptr;
+  if (dbias.has_value()) {
+    check_gpu(*dbias, "dbias");
+    check_dtype(*dbias, at::kFloat, "dbias");
+    TORCH_CHECK(dbias->numel() == 3 * H * 64, "dbias must have 3*H*64 elements");
+    db = dbias->data_ptr<float>();
+  }
   check_hip(llmt::launch_attn_bwd(dout.data_ptr(), qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
-                                  dqkv.data_ptr(), delta.data_ptr<float>(), dq.data_ptr<float>(), (int)B, (int)T,
+                                  dqkv.data_ptr(), delta.data_ptr<float>(), dq.data_ptr<float>(), db, (int)B, (int)T,
                                   (int)H, make_dropout(dropout_p, dropout_seed), cur_stream()),
             "attn_bwd");
   return dqkv;
@@ -401,7 +408,7 @@ TORCH_LIBRARY(llmtrain_hip, m) {
         " int dropout_seed=0) -> ()");
   m.def("attn_fwd(Tensor qkv, int B, int T, int H, float dropout_p=0., int dropout_seed=0) -> (Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, int B, int T, int H, float dropout_p=0.,"
-        " int dropout_seed=0) -> Tensor");
+        " int dropout_seed=0, Tensor(a!)? dbias=None) -> Tensor");
   m.def("dropout_mask(int n, float p, int seed, Tensor like) -> Tensor");
   m.def("wgrad_gemm(Tensor dy, Tensor x, Tensor(a!) c, int split=0, int tile=0) -> ()");
   m.def("sumsq(Tensor x) -> Tensor");

@@ -111,11 +111,12 @@ hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, fl
 // mix32(seed + (b*H + h) * 0x9E3779B9), index q*T + k); lse stays the undropped normaliser
 hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H,
                            DropoutArgs dropout, hipStream_t stream);
-// dqkv [B, T, 3, H, 64] bf16; `delta` [B, H, T] f32 and `dq_part`
+// dqkv [B, T, 3, H, 64] bf16; optional `dbias` [3*H*64] f32 accumulates the column sums of dqkv
+// (the qkv projection's bias gradient); `delta` [B, H, T] f32 and `dq_part`
 // (attn_bwd_workspace_floats(B, T, H) floats) scratch
 long attn_bwd_workspace_floats(int B, int T, int H);
 hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse,
-                           void* dqkv, float* delta, float* dq_part, int B, int T, int H,
-                           DropoutArgs dropout, hipStream_t stream);
+                           void* dqkv, float* delta, float* dq_part, float* dbias, int B, int T,
+                           int H, DropoutArgs dropout, hipStream_t stream);
 
 }  // namespace llmt

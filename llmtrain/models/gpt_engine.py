@@ -319,9 +319,12 @@ class FusedGPTEngine:
             self._wgrad(self._g(blk.attn.out_proj.weight), dy_lp, a.att)
             datt = torch.mm(dy_lp, self._w(blk.attn.out_proj.weight))
             del dy_lp
-            dqkv = ops.attn_bwd(datt, a.qkv, a.att, a.lse, bsz, seqlen, self.n_heads, dropout=st.site(2 + 3 * i))
+            # the qkv-bias gradient (column sums of dqkv) is fused into the attention backward
+            dqkv = ops.attn_bwd(
+                datt, a.qkv, a.att, a.lse, bsz, seqlen, self.n_heads, dropout=st.site(2 + 3 * i),
+                qkv_bias_grad=self._g(blk.attn.qkv_proj.bias),
+            )
             del datt
-            ops.colsum_accum(dqkv, self._g(blk.attn.qkv_proj.bias))
             self._wgrad(self._g(blk.attn.qkv_proj.weight), dqkv, a.h1)
             dh1 = torch.mm(dqkv, self._w(blk.attn.qkv_proj.weight))
             del dqkv

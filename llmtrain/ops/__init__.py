@@ -121,11 +121,16 @@ def attn_fwd(qkv, bsz: int, seqlen: int, n_heads: int, dropout=(0.0, 0)):
     return ref.attn_fwd(qkv, bsz, seqlen, n_heads, p, seed)
 
 
-def attn_bwd(dout, qkv, out, lse, bsz: int, seqlen: int, n_heads: int, dropout=(0.0, 0)):
+def attn_bwd(dout, qkv, out, lse, bsz: int, seqlen: int, n_heads: int, dropout=(0.0, 0), qkv_bias_grad=None):
+    """Attention backward -> packed ``dqkv``; ``qkv_bias_grad`` (fp32 ``[3d]``), when given,
+    accumulates ``colsum(dqkv)`` (fused into the kernels on GPU)."""
     p, seed = dropout
     if _on_gpu(dout):
-        return hip_ops().attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads, p, seed)
-    return ref.attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads, p, seed)
+        return hip_ops().attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads, p, seed, qkv_bias_grad)
+    dqkv = ref.attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads, p, seed)
+    if qkv_bias_grad is not None:
+        ref.colsum_accum(dqkv, qkv_bias_grad)
+    return dqkv
 
 
 def wgrad_accum(dst, dy, x) -> None:

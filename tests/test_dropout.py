@@ -123,7 +123,11 @@ def test_fused_dropout_kernels_on_gpu(gpu_device) -> None:  # type: ignore[no-un
     out_r, lse_r = ref.attn_fwd(qkv, B, T, H, *adrop)
     torch.testing.assert_close(lse_g.cpu(), lse_r, atol=2e-3, rtol=2e-3)
     torch.testing.assert_close(out_g.cpu().float(), out_r.float(), atol=3e-2, rtol=3e-2)
-    dq_g = ops.attn_bwd(dout.to(gpu_device), qkv.to(gpu_device), out_g, lse_g, B, T, H, dropout=adrop).cpu().float()
+    dbias = torch.zeros(3 * 64 * H, device=gpu_device)
+    dq_g = ops.attn_bwd(dout.to(gpu_device), qkv.to(gpu_device), out_g, lse_g, B, T, H, dropout=adrop,
+                        qkv_bias_grad=dbias).cpu().float()
     dq_r = ref.attn_bwd(dout, qkv, out_g.cpu(), lse_g.cpu(), B, T, H, *adrop).float()
     scale = dq_r.abs().max().item()
     assert (dq_g - dq_r).abs().max().item() < 2e-2 * scale
+    want = dq_r.sum(dim=0)  # K part: exactly 0 in exact arithmetic (softmax shift invariance)
+    assert (dbias.cpu() - want).abs().max().item() < 2e-2 * want.abs().max().item()

@@ -179,6 +179,12 @@ def test_attention_fwd_bwd(gpu_device, B, T, H):
     for i, name in enumerate(names):
         scale = r[:, :, i].abs().max().item()
         _close(a[:, :, i], r[:, :, i], 2e-2 * scale, 3e-2, name)
+    # fused qkv-bias gradient (column sums of dqkv) accumulates into an existing buffer
+    dbias = torch.ones(3 * d, device=gpu_device)
+    dqkv2 = hip().attn_bwd(dout, qkv, out, lse, B, T, H, 0.0, 0, dbias)
+    assert torch.equal(dqkv2, dqkv)
+    want = 1.0 + dqkv_r.sum(dim=0)
+    _close(dbias, want, 2e-2 * want.abs().max().item(), 2e-2, "qkv bias grad")
 
 
 def test_attention_causality(gpu_device):

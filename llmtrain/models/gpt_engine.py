@@ -181,6 +181,10 @@ class FusedGPTEngine:
         self.padding_seen = torch.zeros((), dtype=torch.bool, device=self.store.device)
         self._anchor = torch.zeros((), requires_grad=True, device=self.store.device)
         self.wgrad_impl = os.environ.get("LLMTRAIN_WGRAD", "hip")
+        # weight-gradient GEMMs on a second HIP stream, overlapping the dX GEMMs and the
+        # bandwidth-bound backward kernels of the main stream (LLMTRAIN_WGRAD_STREAM=0 disables)
+        self.wgrad_stream_enabled = os.environ.get("LLMTRAIN_WGRAD_STREAM", "1") != "0"
+        self._side: torch.cuda.Stream | None = None
 
     # ------------------------------------------------------------------------------------
 
@@ -197,11 +201,39 @@ class FusedGPTEngine:
     def _wgrad(self, dst: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
         """Block weight gradients: the split-K MFMA kernel (``ops.wgrad_accum``) on GPU — it fills
         the chip on these M-deep reductions where hipBLASLt picks too few tiles — unless
-        ``LLMTRAIN_WGRAD=hipblaslt`` selects the library GEMM for A/B runs."""
-        if dst.is_cuda and dy.dtype == torch.bfloat16 and self.wgrad_impl == "hip":
+        ``LLMTRAIN_WGRAD=hipblaslt`` selects the library GEMM for A/B runs.  On GPU it runs on the
+        side stream after an event on the main stream (``dy``/``x`` are ready); ``record_stream``
+        keeps their memory from being reused by the main stream until the side stream is done."""
+        if not (dst.is_cuda and dy.dtype == torch.bfloat16):
+            accumulate_wgrad(dst, dy, x)
+            return
+        side = self._side_stream()
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                self._wgrad_now(dst, dy, x)
+            dy.record_stream(side)
+            x.record_stream(side)
+        else:
+            self._wgrad_now(dst, dy, x)
+
+    def _wgrad_now(self, dst: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
+        if self.wgrad_impl == "hip":
             ops.wgrad_accum(dst, dy, x)
         else:
             accumulate_wgrad(dst, dy, x)
+
+    def _side_stream(self) -> torch.cuda.Stream | None:
+        if not self.wgrad_stream_enabled or not self.store.device.type == "cuda":
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.store.device)
+        return self._side
+
+    def _join_side(self) -> None:
+        """Main stream waits for every weight-gradient GEMM issued so far."""
+        if self._side is not None:
+            torch.cuda.current_stream().wait_stream(self._side)
 
     def _linear(self, x: torch.Tensor, layer: torch.nn.Linear) -> torch.Tensor:
         w = self._w(layer.weight)
@@ -272,7 +304,17 @@ class FusedGPTEngine:
     # -- backward --------------------------------------------------------------------------
 
     def _notify(self, segment: str) -> None:
-        if self.grad_ready is not None:
+        """A segment's gradients are final: hand it to the data-parallel reducer.  Its bucket holds
+        side-stream (weight) and main-stream (bias, LayerNorm) gradients, so the collective is
+        launched from the side stream after it has caught up with the main stream — RCCL then
+        orders the all-reduce after both without stalling the main stream's next layer."""
+        if self.grad_ready is None:
+            return
+        if self._side is not None:
+            self._side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self._side):
+                self.grad_ready(segment)
+        else:
             self.grad_ready(segment)
 
     def _backward(self, st: _StepState, grad_out: torch.Tensor) -> None:
@@ -341,3 +383,4 @@ class FusedGPTEngine:
             dx, st.ids, self._g(m.token_embedding.weight), self._g(m.position_embedding.weight), dropout=st.site(0)
         )
         self._notify("embed")
+        self._join_side()  # clip / optimizer / loss readers on the main stream see every gradient

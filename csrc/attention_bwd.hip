@@ -41,7 +41,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
                                                          const bf16_raw* __restrict__ out,
                                                          float* __restrict__ delta, float* __restrict__ dbias_v,
                                                          int T, int H) {
-  __shared__ float red[32][65];
+  __shared__ float red[4][kHD];
   const int bh = blockIdx.y;
   const int b = bh / H, h = bh - b * H;
   const int rl = threadIdx.x >> 3, sub = threadIdx.x & 7;
@@ -61,12 +61,21 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
   acc += __shfl_xor(acc, 4, 64);
   if (t < T && sub == 0) delta[(long)bh * T + t] = acc;
   if (dbias_v == nullptr) return;  // uniform: kernel argument
+  // column sums: over the wave's 8 rows with shuffles (lanes sharing `sub`), then the 4 waves
 #pragma unroll
-  for (int i = 0; i < 8; ++i) red[rl][8 * sub + i] = a[i];
+  for (int i = 0; i < 8; ++i) {
+    a[i] += __shfl_xor(a[i], 8, 64);
+    a[i] += __shfl_xor(a[i], 16, 64);
+    a[i] += __shfl_xor(a[i], 32, 64);
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) < 8) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[wv][8 * sub + i] = a[i];
+  }
   __syncthreads();
   if (threadIdx.x < kHD) {
-    float s = 0.f;
-    for (int r = 0; r < 32; ++r) s += red[r][threadIdx.x];
+    const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
     atomicAdd(dbias_v + h * kHD + threadIdx.x, s);
   }
 }

@@ -61,6 +61,9 @@ __global__ __launch_bounds__(kCeThreads) void ce_fwd_bwd_kernel(
   const bool valid = label >= 0 && label < V;
   const float t_label = valid ? scalar_f(z[label]) * kLog2e : 0.f;  // read before any write
 
+  // Only the row's last vector can hold padded columns (Vp - V < 64) and only one vector holds
+  // the label: both are handled per vector, so the per-element loops carry no compares.
+  const int nfull = V >> 3;  // vectors with 8 real columns
   Vec8<T> v[MAXV];
   float m = -INFINITY;
 #pragma unroll
@@ -68,9 +71,14 @@ __global__ __launch_bounds__(kCeThreads) void ce_fwd_bwd_kernel(
     const int c = threadIdx.x + j * kCeThreads;
     if (c < nvec) {
       v[j].load(z + 8 * c);
+      if (c < nfull) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (8 * c + i < V) m = fmaxf(m, v[j].get(i));
+        for (int i = 0; i < 8; ++i) m = fmaxf(m, v[j].get(i));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (8 * c + i < V) m = fmaxf(m, v[j].get(i));
+      }
     }
   }
   const float zmax = block_max<kCeWaves>(m, scratch);
@@ -80,28 +88,35 @@ __global__ __launch_bounds__(kCeThreads) void ce_fwd_bwd_kernel(
   for (int j = 0; j < MAXV; ++j) {
     const int c = threadIdx.x + j * kCeThreads;
     if (c < nvec) {
+      if (c < nfull) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (8 * c + i < V) s += __builtin_amdgcn_exp2f(fmaf(v[j].get(i), kLog2e, -tmax));
+        for (int i = 0; i < 8; ++i) s += __builtin_amdgcn_exp2f(fmaf(v[j].get(i), kLog2e, -tmax));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (8 * c + i < V) s += __builtin_amdgcn_exp2f(fmaf(v[j].get(i), kLog2e, -tmax));
+      }
     }
   }
   const float ssum = block_sum<kCeWaves>(s, scratch);
   const float lse2 = tmax + log2f(ssum);
   const float w = valid ? row_w[row] : 0.f;
+  const int label_vec = valid ? (int)(label >> 3) : -1;
 #pragma unroll
   for (int j = 0; j < MAXV; ++j) {
     const int c = threadIdx.x + j * kCeThreads;
     if (c < nvec) {
+      if (c < nfull) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int col = 8 * c + i;
-        float gval = 0.f;
-        if (col < V) {
-          gval = __builtin_amdgcn_exp2f(fmaf(v[j].get(i), kLog2e, -lse2));
-          if (col == label) gval -= 1.f;
-          gval *= w;
-        }
-        v[j].set(i, gval);
+        for (int i = 0; i < 8; ++i) v[j].set(i, __builtin_amdgcn_exp2f(fmaf(v[j].get(i), kLog2e, -lse2)) * w);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          v[j].set(i, 8 * c + i < V ? __builtin_amdgcn_exp2f(fmaf(v[j].get(i), kLog2e, -lse2)) * w : 0.f);
+      }
+      if (c == label_vec) {  // onehot: recompute the label column exactly, then subtract
+        const int i = (int)(label & 7);
+        v[j].set(i, (__builtin_amdgcn_exp2f(t_label - lse2) - 1.f) * w);  // t_label: read at entry
       }
       v[j].store(z + 8 * c);
     }

@@ -13,9 +13,29 @@ namespace {
 constexpr float kInvSqrt2 = 0.70710678118654752f;
 constexpr float kInvSqrt2Pi = 0.39894228040143268f;
 
-__device__ __forceinline__ float gelu(float u) { return 0.5f * u * (1.f + erff(u * kInvSqrt2)); }
+// Exact-erf GELU (nn.GELU() default) with a cheap erf: Abramowitz & Stegun 7.1.26,
+// |erf error| < 1.5e-7 absolute — it enters GELU and its derivative only through (1 + erf), far
+// below the bf16 rounding of the kernels' outputs — at one v_rcp_f32, one v_exp_f32 and five FMAs
+// instead of ocml's erff.  e = exp(-u^2/2) is shared between erf(u/sqrt2) and the pdf term.
+struct ErfPdf {
+  float erf;  // erf(u / sqrt 2)
+  float e;    // exp(-u^2 / 2)
+};
+__device__ __forceinline__ ErfPdf erf_pdf(float u) {
+  constexpr float kLog2e = 1.4426950408889634f;
+  const float az = fabsf(u) * kInvSqrt2;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(-0.5f * kLog2e * u * u);
+  return {copysignf(fmaf(-p * t, e, 1.f), u), e};
+}
+__device__ __forceinline__ float gelu(float u) { return 0.5f * u * (1.f + erf_pdf(u).erf); }
 __device__ __forceinline__ float gelu_grad(float u) {
-  return 0.5f * (1.f + erff(u * kInvSqrt2)) + u * kInvSqrt2Pi * __expf(-0.5f * u * u);
+  const ErfPdf ep = erf_pdf(u);
+  return fmaf(0.5f, 1.f + ep.erf, u * kInvSqrt2Pi * ep.e);
 }
 
 // 8-wide load/store of either dtype as f32
@@ -66,24 +86,41 @@ __global__ __launch_bounds__(256) void colwise_kernel(const void* __restrict__ a
   const int r0 = blockIdx.y * rows_per_block;
   const int r1 = min(M, r0 + rows_per_block);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // UNROLL rows per iteration: their loads are all issued before the first use, so each wave keeps
+  // UNROLL x (1 or 2) 1-KiB requests in flight instead of one (memory-level parallelism).
+  constexpr int UNROLL = 4;
+  auto row_op = [&](float* x, const float* uu, long i8) {
+    if (OP == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] *= gelu_grad(uu[k]);
+      if (BF16) {  // round first so dbias sums exactly what the next GEMM consumes
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = bf2f(f2bf(x[k]));
+      }
+      st8<BF16>(out, i8, x);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += x[k];
+  };
   if (cv < F8) {
-    for (int r = r0 + wid; r < r1; r += 4) {
-      const long i8 = (long)r * F8 + cv;
-      float x[8];
-      ld8<BF16>(a, i8, x);
-      if (OP == 0) {
-        float uu[8];
-        ld8<BF16>(u, i8, uu);
+    int r = r0 + wid;
+    for (; r + 4 * (UNROLL - 1) < r1; r += 4 * UNROLL) {
+      float x[UNROLL][8], uu[UNROLL][8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) x[k] *= gelu_grad(uu[k]);
-        if (BF16) {  // round first so dbias sums exactly what the next GEMM consumes
-#pragma unroll
-          for (int k = 0; k < 8; ++k) x[k] = bf2f(f2bf(x[k]));
-        }
-        st8<BF16>(out, i8, x);
+      for (int q = 0; q < UNROLL; ++q) {
+        const long i8 = (long)(r + 4 * q) * F8 + cv;
+        ld8<BF16>(a, i8, x[q]);
+        if (OP == 0) ld8<BF16>(u, i8, uu[q]);
       }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += x[k];
+      for (int q = 0; q < UNROLL; ++q) row_op(x[q], uu[q], (long)(r + 4 * q) * F8 + cv);
+    }
+    for (; r < r1; r += 4) {
+      float x[8], uu[8];
+      const long i8 = (long)r * F8 + cv;
+      ld8<BF16>(a, i8, x);
+      if (OP == 0) ld8<BF16>(u, i8, uu);
+      row_op(x, uu, i8);
     }
   }
   if (colsum == nullptr) return;

@@ -85,3 +85,51 @@ def test_trainer_metric_collectives_on_device(nccl_world, in_tmp):
     red = torch.tensor([1.0, 2.0], device=nccl_world, dtype=torch.float64)
     dist.all_reduce(red)
     assert red.tolist() == [1.0, 2.0]
+
+
+def _two_rank_worker(rank: int, world: int, port: int, out_dir: str) -> None:
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from llmtrain.parallel.reducer import FlatDataParallel
+
+    torch.manual_seed(0)
+    model = GPT(vocab_size=512, block_size=128, d_model=256, n_layers=3, n_heads=4, d_ff=1024, dropout=0.0).cuda()
+    model.prepare_runtime(compute_dtype=torch.bfloat16)
+    assert model.engine.wgrad_stream_enabled
+    ddp = FlatDataParallel(model, bucket_cap_mb=1.0)
+    g = torch.Generator().manual_seed(7)
+    batches = [torch.randint(0, 512, (4, 128), generator=g).cuda() for _ in range(2 * world)]
+    mine = batches[2 * rank : 2 * rank + 2]
+    model.flat_store.zero_grad()
+    with ddp.no_sync():
+        (ddp.fused_loss(mine[0], mine[0]) / 2).backward()
+    (ddp.fused_loss(mine[1], mine[1]) / 2).backward()
+    ddp.finish_gradient_sync()
+    torch.cuda.synchronize()
+    torch.save({"grad": model.flat_store.grad.cpu()}, f"{out_dir}/rank{rank}.pt")
+    dist.destroy_process_group()
+
+
+def test_two_ranks_side_stream_reducer_matches_single_process(gpu_device, tmp_path) -> None:  # type: ignore[no-untyped-def]
+    """Two ranks on the one GPU (gloo on CUDA tensors — RCCL refuses two ranks per device) drive the
+    fused engine with its side-stream weight gradients and the bucketed reducer: the averaged
+    gradient equals one process accumulating all four micro-batches."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_two_rank_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)["grad"]
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)["grad"]
+    assert torch.equal(r0, r1)
+    torch.manual_seed(0)
+    solo = GPT(vocab_size=512, block_size=128, d_model=256, n_layers=3, n_heads=4, d_ff=1024, dropout=0.0)
+    solo = solo.to(gpu_device)
+    solo.prepare_runtime(compute_dtype=torch.bfloat16)
+    g = torch.Generator().manual_seed(7)
+    batches = [torch.randint(0, 512, (4, 128), generator=g).to(gpu_device) for _ in range(4)]
+    solo.flat_store.zero_grad()
+    for b in batches:
+        (solo.fused_loss(b, b) / 4).backward()
+    torch.cuda.synchronize()
+    want = solo.flat_store.grad.cpu()
+    assert (r0 - want).abs().max().item() <= 2e-3 * want.abs().max().item()

@@ -65,32 +65,31 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
   const int kv_end = min(T, qb * kQBlk + kQBlk);
   const int ntiles = (kv_end + kKBlk - 1) / kKBlk;
 
-  // register staging of one K/V tile: 512 16-byte chunks each, 2 per thread
-  ushort8_t stage[4];
-  auto load_tile = [&](int tile) {
+  // register staging of K/V tiles TWO tiles ahead (two stage sets): a tile's global loads get two
+  // iterations of compute to land instead of one.  Buffer loads bounded at row T of this (b, h):
+  // keys past the sequence read as zeros without branches.
+  const __amdgpu_buffer_rsrc_t rkv = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)base, (short)0, (int)(((long)T - 1) * row_stride + 3 * kHD * H) * 2, 0x00020000);
+  ushort8_t st0[4], st1[4];
+  auto load_tile = [&](ushort8_t(&st)[4], int tile) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c = threadIdx.x + 256 * i;
       const int r = c >> 3, ch = c & 7;
-      const int key = tile * kKBlk + r;
-      ushort8_t kz = {0, 0, 0, 0, 0, 0, 0, 0}, vz = kz;
-      if (key < T) {
-        const bf16_raw* src = base + (long)key * row_stride + ch * 8;
-        kz = *reinterpret_cast<const ushort8_t*>(src + kHD * H);
-        vz = *reinterpret_cast<const ushort8_t*>(src + 2 * kHD * H);
-      }
-      stage[i] = kz;
-      stage[2 + i] = vz;
+      const int off = (int)(((long)(tile * kKBlk + r) * row_stride + ch * 8 + kHD * H) * 2);
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      st[i] = __builtin_bit_cast(ushort8_t, __builtin_amdgcn_raw_buffer_load_b128(rkv, off, 0, 0));
+      st[2 + i] = __builtin_bit_cast(ushort8_t, __builtin_amdgcn_raw_buffer_load_b128(rkv, off + kHD * H * 2, 0, 0));
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](const ushort8_t(&st)[4], int buf) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c = threadIdx.x + 256 * i;
       const int r = c >> 3, ch = c & 7;
       const int off = tile_chunk_off(r, ch);
-      *reinterpret_cast<ushort8_t*>(&smem[buf][0][off]) = stage[i];
-      *reinterpret_cast<ushort8_t*>(&smem[buf][1][off]) = stage[2 + i];
+      *reinterpret_cast<ushort8_t*>(&smem[buf][0][off]) = st[i];
+      *reinterpret_cast<ushort8_t*>(&smem[buf][1][off]) = st[2 + i];
     }
   };
 
@@ -100,14 +99,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
   float m_run = -INFINITY, l_run = 0.f;
   constexpr float c = 0.125f * 1.4426950408889634f;  // (1/sqrt(64)) * log2(e)
 
-  load_tile(0);
-  store_tile(0);
+  load_tile(st0, 0);
+  store_tile(st0, 0);
   __syncthreads();
+  if (ntiles > 1) load_tile(st1, 1);
+  if (ntiles > 2) load_tile(st0, 2);
 
-  for (int it = 0; it < ntiles; ++it) {
+  // iteration `it` computes from LDS buffer it&1, then stages tile it+1 (held in stage set
+  // (it+1)&1 since two iterations ago) into the other buffer and refills that set with tile it+3
+  auto tile_step = [&](int it, ushort8_t(&st_next)[4]) __attribute__((always_inline)) {
     const int cur = it & 1;
     const bool more = it + 1 < ntiles;
-    if (more) load_tile(it + 1);
     const int kbase = it * kKBlk;
     if (kbase <= q_hi) {
       const bf16_raw* Kt = smem[cur][0];
@@ -182,8 +184,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
         }
       }
     }
-    if (more) store_tile(cur ^ 1);
+    if (more) store_tile(st_next, cur ^ 1);
     __syncthreads();
+    if (it + 3 < ntiles) load_tile(st_next, it + 3);
+  };
+  for (int it = 0; it < ntiles; it += 2) {
+    tile_step(it, st1);
+    if (it + 1 < ntiles) tile_step(it + 1, st0);
   }
 
   if (q < T) {

@@ -83,3 +83,35 @@ def test_trainer_fused_gpu_learns(gpu_device, in_tmp):
     assert result.first_step_loss is not None and result.final_loss < result.first_step_loss - 1.0
     assert result.final_val_loss is not None and result.final_val_loss < math.log(512)
     assert result.peak_memory > 0.0
+
+
+def _gpu_cfg(root: str, max_steps: int, dropout: float = 0.0) -> RunConfig:
+    return RunConfig.model_validate({
+        "schema_version": 1,
+        "run": {"name": "gpu-resume", "device": "cuda", "precision": "bf16", "seed": 5},
+        "model": {"name": "gpt", "vocab_size": 512, "block_size": 128, "d_model": 128, "n_layers": 2,
+                  "n_heads": 2, "d_ff": 512, "dropout": dropout},
+        "data": {"name": "synthetic_tokens", "num_workers": 0, "extra": {"train_sequences": 256, "val_sequences": 16}},
+        "trainer": {"max_steps": max_steps, "micro_batch_size": 8, "grad_accum_steps": 2, "lr": 1e-3,
+                    "warmup_steps": 2, "log_every_steps": 2, "eval_every_steps": 100, "save_every_steps": 3},
+        "ddp": {}, "mlflow": {"enabled": False}, "logging": {"log_to_file": False},
+        "output": {"root_dir": root},
+    })
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.1])
+def test_fused_engine_mid_run_resume(gpu_device, tmp_path, dropout):
+    """BASELINE config 5's mid-run checkpoint + --resume on the fused engine (with grad accumulation
+    and, optionally, fused dropout whose masks derive from the checkpointed torch RNG state): the
+    resumed run continues the interrupted one.  fp32 atomics in the weight-gradient kernels make
+    bf16 runs non-bitwise, hence a small tolerance instead of the CPU test's 1e-5."""
+    from llmtrain.training.trainer import Trainer
+
+    full = Trainer(_gpu_cfg(str(tmp_path / "a"), 8, dropout), run_dir=tmp_path / "a" / "run").fit()
+    part = tmp_path / "b" / "run"
+    Trainer(_gpu_cfg(str(tmp_path / "b"), 8, dropout), run_dir=part).fit(max_steps_override=6)
+    resumed = Trainer(_gpu_cfg(str(tmp_path / "b"), 8, dropout), run_dir=tmp_path / "b" / "run2").fit(
+        resume_from=str(part / "checkpoints")
+    )
+    assert resumed.resumed_from_step == 6 and resumed.final_step == 8
+    assert abs(resumed.final_loss - full.final_loss) <= 2e-3 * abs(full.final_loss)

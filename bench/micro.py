@@ -62,8 +62,12 @@ def gemm(M: int = 32768, only: str = "") -> list[dict]:
                 torch.bmm(dy.view(16, M // 16, N).transpose(1, 2), x.view(16, M // 16, K)).float().sum(0)
             ),
         }
+        bias = torch.randn(N, device=dev, dtype=torch.bfloat16)
+        variants["fwd addmm bias"] = lambda: torch.addmm(bias, x, w.t())
         for vname, fn in variants.items():
             if only == "wgrad" and not ("llmtrain" in vname or "addmm" in vname):
+                continue
+            if only == "fwd" and not (vname.startswith("fwd") or vname.startswith("dX")):
                 continue
             if name == "head" and "llmtrain" in vname:
                 continue  # 3.3 GB dY: beyond the kernel's 32-bit buffer offsets (head uses hipBLASLt)
@@ -71,6 +75,47 @@ def gemm(M: int = 32768, only: str = "") -> list[dict]:
             rows.append({"gemm": name, "variant": vname, "ms": round(ms, 4), "TFLOPs": round(flops / ms / 1e9, 1)})
             print(json.dumps(rows[-1]), flush=True)
         del x, w, dy, acc
+    return rows
+
+
+def fgemm(M: int = 65536) -> list[dict]:
+    """llmtrain fused forward/dX GEMM (csrc/gemm_fused.hip) against hipBLASLt (+ the separate
+    GELU kernels it replaces) on the GPT-2 124M shapes."""
+    from llmtrain.ops import _ext
+
+    _ext.require()
+    ops = torch.ops.llmtrain_hip
+    dev = torch.device("cuda")
+    rows = []
+    shapes = {"qkv": (768, 2304), "out": (768, 768), "fc": (768, 3072), "proj": (3072, 768)}
+    for name, (K, N) in shapes.items():
+        x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+        w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) / K**0.5
+        dy = torch.randn(M, N, device=dev, dtype=torch.bfloat16)
+        bias = torch.randn(N, device=dev, dtype=torch.bfloat16)
+        u = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+        dbk = torch.zeros(K, device=dev)
+        dbn = torch.zeros(N, device=dev)
+        variants = {
+            "fwd hipblaslt addmm": (lambda: torch.addmm(bias, x, w.t()), 2.0 * M * K * N),
+            "fwd llmtrain epi0": (lambda: ops.gemm_fused(x, w, False, 0, bias), 2.0 * M * K * N),
+            "dX hipblaslt mm": (lambda: torch.mm(dy, w), 2.0 * M * K * N),
+            "dX llmtrain epi0": (lambda: ops.gemm_fused(dy, w, True, 0), 2.0 * M * K * N),
+        }
+        if name == "fc":
+            variants["fwd hipblaslt addmm + gelu"] = (
+                lambda: ops.gelu_fwd(torch.addmm(bias, x, w.t())), 2.0 * M * K * N)
+            variants["fwd llmtrain epi1 (bias+gelu)"] = (lambda: ops.gemm_fused(x, w, False, 1, bias), 2.0 * M * K * N)
+        if name == "proj":  # dX of proj: [M,768] @ [768,3072] -> GELU backward on [M,3072]
+            variants["dX hipblaslt mm + gelu_bwd"] = (
+                lambda: ops.gelu_bwd(torch.mm(dy, w), u, dbk), 2.0 * M * K * N)
+            variants["dX llmtrain epi2 (dgelu+dbias)"] = (
+                lambda: ops.gemm_fused(dy, w, True, 2, None, u, dbk), 2.0 * M * K * N)
+        del dbn
+        for vname, (fn, flops) in variants.items():
+            ms = timeit(fn)
+            rows.append({"gemm": name, "variant": vname, "ms": round(ms, 4), "TFLOPs": round(flops / ms / 1e9, 1)})
+            print(json.dumps(rows[-1]), flush=True)
     return rows
 
 
@@ -110,5 +155,9 @@ if __name__ == "__main__":
         gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 32768)
     if what == "wgrad":  # just the weight-gradient variants
         gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 65536, only="wgrad")
+    if what == "fwd":  # forward / dX GEMMs
+        gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 65536, only="fwd")
+    if what == "fgemm":
+        fgemm(int(sys.argv[2]) if len(sys.argv) > 2 else 65536)
     if what in ("attn", "all"):
         attn()

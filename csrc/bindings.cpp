@@ -341,6 +341,65 @@ void wgrad_gemm(const Tensor& dy, const Tensor& x, Tensor c, int64_t split, int6
             "wgrad_gemm");
 }
 
+// ---- fused forward / dX GEMM ------------------------------------------------------------------
+// out = epi(a @ op(b)): b is [N, K] (weight, forward) or, with b_kn, [K, N] (weight in dX = dy @ W).
+// epilogue 0 -> (out, None); 1 -> (u, gelu(u)); 2 -> (du = acc * gelu'(u), None) with dbias += colsum.
+std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tensor& b, bool b_kn, int64_t epilogue,
+                                                     const c10::optional<Tensor>& bias, const c10::optional<Tensor>& u,
+                                                     c10::optional<Tensor> dbias) {
+  check_gpu(a, "a");
+  check_gpu(b, "b");
+  check_dtype(a, at::kBFloat16, "a");
+  check_dtype(b, at::kBFloat16, "b");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm_fused: 2D operands");
+  const int64_t M = a.size(0), K = a.size(1);
+  const int64_t N = b_kn ? b.size(1) : b.size(0);
+  TORCH_CHECK((b_kn ? b.size(0) : b.size(1)) == K, "gemm_fused: inner dimensions differ");
+  TORCH_CHECK(K % 32 == 0 && K >= 128 && N % 8 == 0, "gemm_fused: needs K % 32 == 0, K >= 128, N % 8 == 0");
+  TORCH_CHECK(epilogue >= 0 && epilogue <= 2, "gemm_fused: epilogue must be 0, 1 or 2");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  llmt::GemmFusedArgs g;
+  g.a = a.data_ptr();
+  g.lda = (int)K;
+  g.b = b.data_ptr();
+  g.ldb = (int)b.size(1);
+  g.b_kn = b_kn;
+  g.M = (int)M;
+  g.N = (int)N;
+  g.K = (int)K;
+  g.epilogue = (int)epilogue;
+  Tensor out = at::empty({M, N}, a.options());
+  c10::optional<Tensor> out2;
+  g.c = out.data_ptr();
+  g.ldc = (int)N;
+  if (bias.has_value() && epilogue != 2) {
+    check_gpu(*bias, "bias");
+    check_dtype(*bias, at::kBFloat16, "bias");
+    TORCH_CHECK(bias->numel() == N, "gemm_fused: bias must have N elements");
+    g.bias = bias->data_ptr();
+  }
+  if (epilogue == 1) {
+    out2 = at::empty({M, N}, a.options());
+    g.c2 = out2->data_ptr();
+  }
+  if (epilogue == 2) {
+    TORCH_CHECK(u.has_value(), "gemm_fused: epilogue 2 needs u");
+    check_gpu(*u, "u");
+    check_dtype(*u, at::kBFloat16, "u");
+    TORCH_CHECK(u->dim() == 2 && u->size(0) == M && u->size(1) == N, "gemm_fused: u must be [M, N]");
+    g.u = u->data_ptr();
+    g.ldu = (int)N;
+    if (dbias.has_value()) {
+      check_gpu(*dbias, "dbias");
+      check_dtype(*dbias, at::kFloat, "dbias");
+      TORCH_CHECK(dbias->numel() == N, "gemm_fused: dbias must have N elements");
+      g.dbias = dbias->data_ptr<float>();
+    }
+  }
+  if (M > 0) check_hip(llmt::launch_gemm_fused(g, cur_stream()), "gemm_fused");
+  return {out, out2};
+}
+
 // ---- optimizer -------------------------------------------------------------------------------
 Tensor sumsq(const Tensor& x) {
   check_gpu(x, "x");
@@ -411,6 +470,8 @@ TORCH_LIBRARY(llmtrain_hip, m) {
         " int dropout_seed=0, Tensor(a!)? dbias=None) -> Tensor");
   m.def("dropout_mask(int n, float p, int seed, Tensor like) -> Tensor");
   m.def("wgrad_gemm(Tensor dy, Tensor x, Tensor(a!) c, int split=0, int tile=0) -> ()");
+  m.def("gemm_fused(Tensor a, Tensor b, bool b_kn, int epilogue, Tensor? bias=None, Tensor? u=None,"
+        " Tensor(a!)? dbias=None) -> (Tensor, Tensor?)");
   m.def("sumsq(Tensor x) -> Tensor");
   m.def("adamw_flat(Tensor(a!) param, Tensor grad, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor(d!)? shadow,"
         " float lr, float beta1, float beta2, float eps, float weight_decay, int step, Tensor? grad_scale) -> ()");
@@ -429,6 +490,7 @@ TORCH_LIBRARY_IMPL(llmtrain_hip, CUDA, m) {
   m.impl("attn_bwd", &attn_bwd);
   m.impl("dropout_mask", &dropout_mask);
   m.impl("wgrad_gemm", &wgrad_gemm);
+  m.impl("gemm_fused", &gemm_fused);
   m.impl("sumsq", &sumsq);
   m.impl("adamw_flat", &adamw_flat);
 }

@@ -1,0 +1,431 @@
+// Forward / data-gradient GEMM with fused epilogues for gfx950:
+//   C[M, N] (bf16) = epilogue( A[M, K] · op(B) )
+//   A  bf16 row-major [M, lda], K contiguous (activations);
+//   B  bf16 either [N, ldb] K contiguous ("NT": nn.Linear weight, forward y = x W^T) or
+//      [K, ldb] N contiguous ("NN": the same weight in the data-gradient dX = dY W).
+// Epilogues (EPI):
+//   0  C = bf16(acc + bias)                      (bias optional)
+//   1  U = bf16(acc + bias), C2 = bf16(gelu(U))  (fc forward: pre-activation kept for backward)
+//   2  C = bf16(acc * gelu'(U)), dbias += colsum(C)   (proj dX: GELU backward + fc bias grad)
+//
+// Why: in the GPT MLP (reference models/gpt.py:94-105, nn.Linear -> nn.GELU -> nn.Linear) the
+// library GEMM writes the pre-activation, a separate pass reads it and writes gelu(u), and in the
+// backward a third pass reads dg and u to form du and its column sums — 3 x 400 MB of extra HBM
+// traffic per layer at GPT-2 124M / 64K tokens.  Here those passes ride in the GEMM epilogue.
+//
+// Structure (MI355X playbook: LDS-DMA ring, counted vmcnt + raw barrier, XCD-aware persistent
+// tiles; shared building blocks in gemm_common.h):
+//  * 256x256 output tiles, 4 waves (2x2) of 128x128 = 4x4 v_mfma_f32_32x32x16_bf16 accumulators
+//    (256 fp32 per lane in AGPRs), one 256-thread workgroup per CU;
+//  * PERSISTENT: min(#tiles, #CUs) workgroups; each XCD owns a contiguous range of tiles
+//    (m-major, so the workgroups running together on one XCD share A strips in its L2) and the
+//    32 workgroups of an XCD stride through it.  The K stages of ALL of a workgroup's tiles form
+//    one stream through a 4-slot LDS ring (3 stages in flight), so the next tile's first stages
+//    load while this tile's epilogue runs;
+//  * A image [256 m][32 k] and NT B image [256 n][32 k]: 64-byte rows, 16-byte chunks swizzled
+//    by (row >> 2) & 3 so each ds_read_b128 lane group covers all 64 banks; fragments are
+//    direct 16-byte reads.  NN B image [32 k][256 n] with the wgrad swizzle, read transposed
+//    (ds_read_b64_tr_b16);
+//  * MFMA srcA = B fragment, srcB = A fragment, so a lane's accumulator column is one output ROW
+//    and its registers run along N in groups of 4 — the epilogue stages each 32x64 piece through
+//    a per-wave XOR-swizzled fp32 LDS image (no cross-wave sync) and writes 16-byte row
+//    segments with buffer stores (out-of-range lanes get an offset past the descriptor, so the
+//    store count is branch-free and known: the counted waits after an epilogue rely on it).
+#include <cstdlib>
+
+#include "common.h"
+#include "gemm_common.h"
+#include "kernels.h"
+
+namespace llmt {
+namespace fgemm {
+
+using namespace gemm;
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 256, BN = 256, BK = 32, NSLOT = 4, kThreads = 256;
+constexpr int kAElems = BM * BK;                // [256][32]
+constexpr int kBElems = BN * BK;                // [256][32] or [32][256]
+constexpr int kSlotElems = kAElems + kBElems;   // 32 KiB
+constexpr int kDmaA = kAElems * 2 / 1024 / 4;   // 1-KiB DMA ops per wave per stage (4)
+constexpr int kDmaB = kBElems * 2 / 1024 / 4;   // (4)
+constexpr int P = kDmaA + kDmaB;                // 8
+constexpr int kEpiFloats = 32 * 64;             // per-wave fp32 staging image [32][64]
+constexpr int kSmemElems = NSLOT * kSlotElems + 4 * kEpiFloats * 2;  // 160 KiB
+constexpr int kOob = 0x7ffffff0;                // buffer offset past any descriptor: dropped / 0
+
+constexpr float kInvSqrt2 = 0.70710678118654752f;
+constexpr float kInvSqrt2Pi = 0.39894228040143268f;
+
+// exact-erf GELU and derivative (same A&S 7.1.26 erf as elementwise.hip, |err| < 1.5e-7)
+struct ErfPdf {
+  float erf, e;
+};
+__device__ __forceinline__ ErfPdf erf_pdf(float u) {
+  constexpr float kLog2e = 1.4426950408889634f;
+  const float az = fabsf(u) * kInvSqrt2;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(-0.5f * kLog2e * u * u);
+  return {copysignf(fmaf(-p * t, e, 1.f), u), e};
+}
+__device__ __forceinline__ float gelu(float u) { return 0.5f * u * (1.f + erf_pdf(u).erf); }
+__device__ __forceinline__ float gelu_grad(float u) {
+  const ErfPdf ep = erf_pdf(u);
+  return fmaf(0.5f, 1.f + ep.erf, u * kInvSqrt2Pi * ep.e);
+}
+
+// VMEM ops each epilogue issues unconditionally (a lower bound is what the counted waits need)
+template <int EPI>
+struct EpiOps {
+  static constexpr int value = EPI == 0 ? 32 : 64;
+};
+
+// Wait until the stage `n` stages before the newest issued one has landed, then barrier.
+// `post`: an epilogue's S VMEM ops were issued after the newest stage (in-order VM counter).
+template <int S>
+__device__ __forceinline__ void wait_stage(int n, bool post) {
+  constexpr int s2 = 2 * P + S > 63 ? 63 : 2 * P + S;
+  constexpr int s1 = P + S > 63 ? 63 : P + S;
+  if (n >= 2) {
+    if (post) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(s2) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * P) : "memory");
+  } else if (n == 1) {
+    if (post) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(s1) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(P) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+}
+
+// one 256-byte LDS-DMA op (4 bytes per lane), M0 saved/restored like dma16
+__device__ __forceinline__ void dma4(unsigned lds_dst, int voff, __amdgpu_buffer_rsrc_t rsrc, int soff) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %[keep], m0\n\t"
+      "s_nop 4\n\t"
+      "s_mov_b32 m0, %[dst]\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dword %[v], %[r], %[so] offen lds\n\t"
+      "s_mov_b32 m0, %[keep]"
+      : [keep] "=&s"(keep)
+      : [dst] "s"(lds_dst), [v] "v"(voff), [r] "s"(rsrc), [so] "s"(soff)
+      : "memory");
+}
+
+__device__ __forceinline__ bf16x8 lds_b128(const bf16_raw* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+// element offset of (row, 16-byte chunk c) in a [rows][32] image swizzled by (row >> 2) & 3
+__device__ __forceinline__ int k32_off(int row, int c) { return row * 32 + 8 * (c ^ ((row >> 2) & 3)); }
+
+struct Args {
+  const bf16_raw* A;
+  const bf16_raw* B;
+  bf16_raw* C;
+  bf16_raw* C2;          // EPI 1: gelu output
+  const bf16_raw* bias;  // EPI 0/1 (optional for 0)
+  const bf16_raw* U;     // EPI 2: pre-activation
+  float* dbias;          // EPI 2: column sums (optional)
+  int lda, ldb, ldc, ldu;
+  int M, N, K;
+  int tiles_n, ntiles, nwg;
+};
+
+template <bool NN, int EPI>
+__global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
+  __shared__ __attribute__((aligned(16))) bf16_raw smem[kSmemElems];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // ---- this workgroup's tiles: XCD-contiguous range, strided by the XCD's workgroup count
+  const int L = blockIdx.x, xcd = L & 7, jx = L >> 3;
+  const int wgx = (p.nwg - xcd + 7) >> 3;
+  const int q = p.ntiles >> 3, r = p.ntiles & 7;
+  const int cnt = q + (xcd < r ? 1 : 0);
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  const int my_tiles = jx < cnt ? (cnt - jx + wgx - 1) / wgx : 0;
+  if (my_tiles == 0) return;
+  const int nst = p.K / BK;
+  const int total = my_tiles * nst;
+
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.M * p.lda * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.B, (short)0, (NN ? p.K : p.N) * p.ldb * 2, 0x00020000);
+
+  // per-lane DMA source offsets (bytes, relative to the stage's scalar offset)
+  int va[kDmaA], vb[kDmaB];
+#pragma unroll
+  for (int j = 0; j < kDmaA; ++j) {  // A image: 16 rows of 64 B per op
+    const int row = (wave * kDmaA + j) * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ ((row >> 2) & 3);
+    va[j] = (row * p.lda + 8 * c) * 2;
+  }
+#pragma unroll
+  for (int j = 0; j < kDmaB; ++j) {
+    if (NN) {  // [32 k][256 n]: 2 rows of 512 B per op, wgrad swizzle
+      const int row = (wave * kDmaB + j) * 2 + (lane >> 5);
+      const int c = (lane & 31) ^ ((row & 3) << 2);
+      vb[j] = (row * p.ldb + 8 * c) * 2;
+    } else {
+      const int row = (wave * kDmaB + j) * 16 + (lane >> 2);
+      const int c = (lane & 3) ^ ((row >> 2) & 3);
+      vb[j] = (row * p.ldb + 8 * c) * 2;
+    }
+  }
+  const unsigned lds_base = (unsigned)(unsigned long)(lds_void*)smem;
+
+  float* epi = reinterpret_cast<float*>(smem + NSLOT * kSlotElems) + wave * kEpiFloats;
+  const unsigned epi_lds = (unsigned)(unsigned long)(lds_void*)epi;
+  const bool kBiasDma = EPI != 2 && p.bias != nullptr;
+  const __amdgpu_buffer_rsrc_t rbias = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(kBiasDma ? p.bias : p.A), (short)0, kBiasDma ? p.N * 2 : 0, 0x00020000);
+
+  // issue cursor (stage stream over this workgroup's tiles)
+  int is_s = 0, is_t = 0, is_m0 = 0, is_n0 = 0;
+  auto tile_origin = [&](int t, int& m0, int& n0) {
+    const int w = base + jx + t * wgx;
+    const int mt = w / p.tiles_n;
+    m0 = mt * BM;
+    n0 = (w - mt * p.tiles_n) * BN;
+  };
+  tile_origin(0, is_m0, is_n0);
+  auto issue = [&](int g) {
+    const unsigned slot = lds_base + (unsigned)((g % NSLOT) * kSlotElems * 2);
+    const int kk = is_s * BK;
+    const int soa = (is_m0 * p.lda + kk) * 2;
+    const int sob = NN ? (kk * p.ldb + is_n0) * 2 : (is_n0 * p.ldb + kk) * 2;
+#pragma unroll
+    for (int j = 0; j < kDmaA; ++j) dma16(slot + (wave * kDmaA + j) * 1024, va[j], ra, soa);
+#pragma unroll
+    for (int j = 0; j < kDmaB; ++j) dma16(slot + kAElems * 2 + (wave * kDmaB + j) * 1024, vb[j], rb, sob);
+    if (kBiasDma && is_s == nst - 1) {
+      // the tile's bias (this wave's 128 columns, bf16) rides with its last K stage into the head
+      // of the wave's epilogue staging image: landed by that stage's wait, read before staging
+      dma4(epi_lds, lane * 4, rbias, (is_n0 + wn * 128) * 2);
+    }
+    if (++is_s == nst) {
+      is_s = 0;
+      if (++is_t < my_tiles) tile_origin(is_t, is_m0, is_n0);
+    }
+  };
+
+  const __amdgpu_buffer_rsrc_t rc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.C, (short)0, p.M * p.ldc * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rc2 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(EPI == 1 ? p.C2 : p.C), (short)0, p.M * p.ldc * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(EPI == 2 ? p.U : p.C), (short)0, p.M * (EPI == 2 ? p.ldu : p.ldc) * 2, 0x00020000);
+
+#pragma unroll
+  for (int g = 0; g < NSLOT - 1; ++g)
+    if (g < total) issue(g);
+
+  int g = 0;  // global stage index of the stream
+  for (int t = 0; t < my_tiles; ++t) {
+    f32x16 acc[4][4];  // [n-tile a][m-tile b]
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = 0.f;
+
+    for (int s = 0; s < nst; ++s, ++g) {
+      // the first NSLOT-1 waits of a tile after the first follow the previous tile's epilogue
+      wait_stage<EpiOps<EPI>::value>(min(total - 1 - g, NSLOT - 2), t > 0 && s < NSLOT - 1);
+      if (g + NSLOT - 1 < total) issue(g + NSLOT - 1);
+      const bf16_raw* aimg = smem + (g % NSLOT) * kSlotElems;
+      const bf16_raw* bimg = aimg + kAElems;
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        const int c = 2 * ks + (lane >> 5);
+        bf16x8 af[4], bfr[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) af[b] = lds_b128(aimg + k32_off(wm * 128 + 32 * b + (lane & 31), c));
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          if (NN) bfr[a] = tr_frag<BN>(bimg, 16 * ks, wn * 128 + 32 * a, lane);
+          else bfr[a] = lds_b128(bimg + k32_off(wn * 128 + 32 * a + (lane & 31), c));
+        }
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[a], af[b], acc[a][b], 0, 0, 0);
+      }
+    }
+
+    // ---------------- epilogue of tile t ----------------
+    int m0, n0;
+    tile_origin(t, m0, n0);
+    const int mw = m0 + wm * 128, nw = n0 + wn * 128;
+    const int q8 = lane & 7;  // this lane's 8-column group within a 64-column half
+    float bias_f[2][8];
+    float csum[2][8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        bias_f[h][k] = 0.f;
+        csum[h][k] = 0.f;
+      }
+    if (kBiasDma) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const ushort8_t bv = *reinterpret_cast<const ushort8_t*>(reinterpret_cast<const bf16_raw*>(epi) + 64 * h + 8 * q8);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) bias_f[h][k] = bf2f(bv[k]);
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        __builtin_amdgcn_sched_barrier(0);
+        // registers -> LDS image [32 m][64 n] fp32, 16-byte chunk index XOR (row & 7)
+        const int row = lane & 31;
+#pragma unroll
+        for (int a2 = 0; a2 < 2; ++a2) {
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            const int ch = 8 * a2 + 2 * gq + (lane >> 5);
+            const f32x16& v = acc[2 * h + a2][b];
+            *reinterpret_cast<float4_t*>(epi + row * 64 + 4 * (ch ^ (row & 7))) =
+                float4_t{v[4 * gq], v[4 * gq + 1], v[4 * gq + 2], v[4 * gq + 3]};
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // wave-local: LDS executes a wave's ops in order
+        float vals[4][8];
+        int off[4];
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          const int R = 8 * it + (lane >> 3);
+          const float4_t lo = *reinterpret_cast<const float4_t*>(epi + R * 64 + 4 * ((2 * q8) ^ (R & 7)));
+          const float4_t hi = *reinterpret_cast<const float4_t*>(epi + R * 64 + 4 * ((2 * q8 + 1) ^ (R & 7)));
+          vals[it][0] = lo[0]; vals[it][1] = lo[1]; vals[it][2] = lo[2]; vals[it][3] = lo[3];
+          vals[it][4] = hi[0]; vals[it][5] = hi[1]; vals[it][6] = hi[2]; vals[it][7] = hi[3];
+          const int m = mw + 32 * b + R, n = nw + 64 * h + 8 * q8;
+          off[it] = (m < p.M && n < p.N) ? (m * p.ldc + n) * 2 : kOob;
+        }
+        asm volatile("" ::: "memory");
+        if (EPI == 2) {
+          u32x4 uraw[4];
+#pragma unroll
+          for (int it = 0; it < 4; ++it) {
+            const int R = 8 * it + (lane >> 3);
+            const int m = mw + 32 * b + R, n = nw + 64 * h + 8 * q8;
+            const int uoff = (m < p.M && n < p.N) ? (m * p.ldu + n) * 2 : kOob;
+            uraw[it] = __builtin_amdgcn_raw_buffer_load_b128(ru, uoff, 0, 0);
+          }
+#pragma unroll
+          for (int it = 0; it < 4; ++it) {
+            __builtin_amdgcn_sched_barrier(0);  // one row of 8 at a time: bounded VGPR pressure
+            const ushort8_t uv = __builtin_bit_cast(ushort8_t, uraw[it]);
+            float o[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              o[k] = bf2f(f2bf(vals[it][k] * gelu_grad(bf2f(uv[k]))));
+              csum[h][k] += o[k];
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(o)), rc, off[it], 0, 0);
+            // pin the running sums here: left alone, hipcc sinks all 128 adds to the end of the
+            // epilogue and keeps every product live (spills)
+            asm volatile("" : "+v"(csum[h][0]), "+v"(csum[h][1]), "+v"(csum[h][2]), "+v"(csum[h][3]),
+                         "+v"(csum[h][4]), "+v"(csum[h][5]), "+v"(csum[h][6]), "+v"(csum[h][7]));
+          }
+        } else {
+#pragma unroll
+          for (int it = 0; it < 4; ++it) {
+            float o[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) o[k] = vals[it][k] + bias_f[h][k];
+            const ushort8_t ov = pack8(o);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ov), rc, off[it], 0, 0);
+            if (EPI == 1) {
+#pragma unroll
+              for (int k = 0; k < 8; ++k) o[k] = gelu(bf2f(ov[k]));
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(o)), rc2, off[it], 0, 0);
+            }
+          }
+        }
+      }
+    }
+    if (EPI == 2 && p.dbias != nullptr) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float s = csum[h][k];
+          s += __shfl_xor(s, 8, 64);
+          s += __shfl_xor(s, 16, 64);
+          s += __shfl_xor(s, 32, 64);
+          csum[h][k] = s;
+        }
+      if (lane < 8) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int n = nw + 64 * h + 8 * q8;
+          if (n < p.N) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) atomicAdd(p.dbias + n + k, csum[h][k]);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <bool NN, int EPI>
+void launch_one(const Args& a, hipStream_t stream) {
+  hipLaunchKernelGGL((gemm_fused_kernel<NN, EPI>), dim3(a.nwg), dim3(kThreads), 0, stream, a);
+}
+
+}  // namespace fgemm
+
+hipError_t launch_gemm_fused(const GemmFusedArgs& g, hipStream_t stream) {
+  using namespace fgemm;
+  if (g.M <= 0 || g.N <= 0) return hipSuccess;
+  if (g.K < 4 * BK || g.K % BK || g.N % 8 || g.lda % 8 || g.ldb % 8 || g.ldc % 8) return hipErrorInvalidValue;
+  if (g.epilogue < 0 || g.epilogue > 2) return hipErrorInvalidValue;
+  if (g.epilogue == 1 && g.c2 == nullptr) return hipErrorInvalidValue;
+  if (g.epilogue == 2 && (g.u == nullptr || g.ldu % 8)) return hipErrorInvalidValue;
+  // 32-bit signed buffer offsets over every operand
+  const long long lim = (1LL << 31) - 64;
+  if ((long long)g.M * g.lda * 2 >= lim || (long long)g.M * g.ldc * 2 >= lim ||
+      (long long)(g.b_kn ? g.K : g.N) * g.ldb * 2 >= lim || (long long)g.M * g.ldu * 2 >= lim)
+    return hipErrorInvalidValue;
+  Args a;
+  a.A = (const bf16_raw*)g.a;
+  a.B = (const bf16_raw*)g.b;
+  a.C = (bf16_raw*)g.c;
+  a.C2 = (bf16_raw*)g.c2;
+  a.bias = (const bf16_raw*)g.bias;
+  a.U = (const bf16_raw*)g.u;
+  a.dbias = g.dbias;
+  a.lda = g.lda;
+  a.ldb = g.ldb;
+  a.ldc = g.ldc;
+  a.ldu = g.ldu;
+  a.M = g.M;
+  a.N = g.N;
+  a.K = g.K;
+  a.tiles_n = (g.N + BN - 1) / BN;
+  a.ntiles = ((g.M + BM - 1) / BM) * a.tiles_n;
+  const int ncu = gemm::cu_count();
+  a.nwg = a.ntiles < ncu ? a.ntiles : ncu;
+  switch (g.epilogue * 2 + (g.b_kn ? 1 : 0)) {
+    case 0: launch_one<false, 0>(a, stream); break;
+    case 1: launch_one<true, 0>(a, stream); break;
+    case 2: launch_one<false, 1>(a, stream); break;
+    case 3: launch_one<true, 1>(a, stream); break;
+    case 4: launch_one<false, 2>(a, stream); break;
+    default: launch_one<true, 2>(a, stream); break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace llmt

@@ -40,17 +40,13 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "gemm_common.h"
 #include "kernels.h"
 
 namespace llmt {
 namespace wgrad {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef short short4v __attribute__((ext_vector_type(4)));
-typedef short short8v __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef __attribute__((address_space(3))) short4v lds_short4;
-typedef __attribute__((address_space(3))) void lds_void;
+using namespace gemm;
 
 constexpr int BM = 32, NSLOT = 4;
 constexpr int kThreads = 256;
@@ -67,49 +63,6 @@ struct Cfg {
   static constexpr int kMinBlocks = (TN * TK >= 16) ? 1 : 2;
 };
 
-template <int W>
-__device__ __forceinline__ int swz_off(int row, int col) {  // element offset in a [rows][W] image
-  return row * W + ((((col >> 3) ^ ((row & 3) << 2))) << 3) + (col & 7);
-}
-
-// 32x32x16 operand with k running down the rows: lane l -> column col0 + (l & 31),
-// elements j = 0..7 -> rows row0 + 8*(l >> 5) + j
-template <int W>
-__device__ __forceinline__ bf16x8 tr_frag(const bf16_raw* tile, int row0, int col0, int lane) {
-  const int i = lane & 15;
-  const int row = row0 + 8 * (lane >> 5) + (i >> 2);
-  const int col = col0 + 16 * ((lane >> 4) & 1) + 4 * (i & 3);
-  const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(tile + swz_off<W>(row, col)));
-  const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(tile + swz_off<W>(row + 4, col)));
-  const short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// "stage s landed for this wave" (n later stages, P DMA ops each, may stay in flight) followed
-// by the workgroup barrier, in ONE asm statement with a memory clobber so no LDS read can be
-// scheduled between the wait and the barrier.
-template <int P>
-__device__ __forceinline__ void wait_stage_and_barrier(int n) {
-  if (n >= 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * P) : "memory");
-  else if (n == 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(P) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-// one 1-KiB LDS-DMA op: M0 (the LDS destination base) is saved/restored inside the statement
-__device__ __forceinline__ void dma16(unsigned lds_dst, int voff, __amdgpu_buffer_rsrc_t rsrc, int soff) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %[keep], m0\n\t"
-      "s_nop 4\n\t"
-      "s_mov_b32 m0, %[dst]\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %[v], %[r], %[so] offen lds\n\t"
-      "s_mov_b32 m0, %[keep]"
-      : [keep] "=&s"(keep)
-      : [dst] "s"(lds_dst), [v] "v"(voff), [r] "s"(rsrc), [so] "s"(soff)
-      : "memory");
-}
-
 template <int TN, int TK>
 __global__ __launch_bounds__(kThreads, (Cfg<TN, TK>::kMinBlocks)) void wgrad_kernel(
     const bf16_raw* __restrict__ A, int lda, const bf16_raw* __restrict__ B, int ldb, float* __restrict__ C,
@@ -120,8 +73,7 @@ __global__ __launch_bounds__(kThreads, (Cfg<TN, TK>::kMinBlocks)) void wgrad_ker
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
   // XCD-aware bijective remap: the 1/8 of the grid dispatched to one XCD gets contiguous work
-  const int L = blockIdx.x, q = nwg >> 3, r = nwg & 7, xcd = L & 7;
-  const int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+  const int w = xcd_remap(blockIdx.x, nwg);
   const int chunk = w / tiles, tile = w - chunk * tiles;
   const int tile_n = tile / tiles_k, tile_k = tile - tile_n * tiles_k;
   const int n0 = tile_n * G::BN, k0 = tile_k * G::BK;
@@ -253,16 +205,6 @@ Plan plan_for(int tile, int M, int N, int K, int split_req, int ncu) {
   return p;
 }
 
-int cu_count() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-  }
-  return n;
-}
-
 }  // namespace wgrad
 
 hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N,
@@ -276,7 +218,7 @@ hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, fl
     }();
     tile = forced;
   }
-  const int ncu = wgrad::cu_count();
+  const int ncu = gemm::cu_count();
   wgrad::Plan p;
   if (tile == 128 || tile == 256) {
     p = wgrad::plan_for(tile, M, N, K, split, ncu);

@@ -104,6 +104,29 @@ hipError_t launch_sumsq(const float* x, long long n, float* partials, float* out
 hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N,
                              int K, int split, int tile, hipStream_t stream);
 
+// ---- forward / data-gradient GEMM with fused epilogues (bf16 in, fp32 accumulate, bf16 out)
+// C[M, N] = epi(A[M, K] . op(B)); B is [N, ldb] (K contiguous, b_kn = false) or [K, ldb]
+// (N contiguous, b_kn = true).  epilogue 0: C = acc + bias (bias optional);
+// 1: C = acc + bias (pre-activation), c2 = gelu(C); 2: C = acc * gelu'(u), dbias += colsum(C).
+// c2 shares C's leading dimension.  K % 32 == 0, K >= 128, N % 8 == 0, leading dimensions % 8 == 0.
+struct GemmFusedArgs {
+  const void* a = nullptr;
+  int lda = 0;
+  const void* b = nullptr;
+  int ldb = 0;
+  bool b_kn = false;
+  void* c = nullptr;
+  int ldc = 0;
+  void* c2 = nullptr;
+  const void* bias = nullptr;
+  const void* u = nullptr;
+  int ldu = 0;
+  float* dbias = nullptr;
+  int M = 0, N = 0, K = 0;
+  int epilogue = 0;
+};
+hipError_t launch_gemm_fused(const GemmFusedArgs& args, hipStream_t stream);
+
 // ---- causal flash attention (head_dim 64) ----------------------------------------------
 // qkv [B, T, 3, H, 64] bf16 (the packed projection output), out [B, T, H, 64] bf16,
 // lse [B, H, T] f32 (natural-log normaliser).

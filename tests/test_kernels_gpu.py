@@ -219,3 +219,58 @@ def test_wgrad_gemm(gpu_device, M, N, K, lda, tile):
     c2 = torch.zeros(N, K, device=gpu_device)
     hip().wgrad_gemm(dy, x, c2, 3, tile)
     _close(c2, dy.float().t() @ x.float(), 1e-3 * scale, 1e-3, "wgrad split=3")
+
+
+# ---- fused forward / dX GEMM (csrc/gemm_fused.hip) -------------------------------------------
+GEMM_SHAPES = [(4096, 3072, 768), (8192, 3072, 768), (513, 768, 3072), (1000, 200, 128), (300, 2304, 768)]
+
+
+def _gemm_operands(M, N, K, b_kn, dev, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    a = (torch.randn(M, K, generator=g) / math.sqrt(K)).to(dev, torch.bfloat16)
+    w = torch.randn(N, K, generator=g).to(dev, torch.bfloat16)  # nn.Linear weight [out, in]
+    b = w.t().contiguous() if b_kn else w  # b_kn: the [K, N] operand of dX = dY @ W
+    bias = (0.1 * torch.randn(N, generator=g)).to(dev, torch.bfloat16)
+    return a, w, b, bias
+
+
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+@pytest.mark.parametrize("b_kn", [False, True])
+def test_gemm_fused_bias(gpu_device, M, N, K, b_kn):
+    a, w, b, bias = _gemm_operands(M, N, K, b_kn, gpu_device, M + N + K)
+    out, none = hip().gemm_fused(a, b, b_kn, 0, bias)
+    assert none is None
+    ref_out = a.float() @ w.float().t() + bias.float()
+    _close(out, ref_out, 2e-2, 1e-2, "gemm+bias")
+    out_nb, _ = hip().gemm_fused(a, b, b_kn, 0)
+    _close(out_nb, a.float() @ w.float().t(), 2e-2, 1e-2, "gemm")
+    again, _ = hip().gemm_fused(a, b, b_kn, 0, bias)
+    assert torch.equal(out, again), "gemm_fused is not deterministic (pipeline race?)"
+
+
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+@pytest.mark.parametrize("b_kn", [False, True])
+def test_gemm_fused_bias_gelu(gpu_device, M, N, K, b_kn):
+    a, w, b, bias = _gemm_operands(M, N, K, b_kn, gpu_device, 3 * M + K)
+    u, gl = hip().gemm_fused(a, b, b_kn, 1, bias)
+    u_ref = a.float() @ w.float().t() + bias.float()
+    _close(u, u_ref, 2e-2, 1e-2, "u")
+    # GELU is applied to the bf16 pre-activation the backward will see
+    _close(gl, torch.nn.functional.gelu(u.float()), 1e-2, 1e-2, "gelu(u)")
+
+
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+@pytest.mark.parametrize("b_kn", [True, False])
+def test_gemm_fused_dgelu(gpu_device, M, N, K, b_kn):
+    a, w, b, _ = _gemm_operands(M, N, K, b_kn, gpu_device, 5 * M + N)
+    g = torch.Generator(device="cpu").manual_seed(11)
+    u = (2 * torch.randn(M, N, generator=g)).to(gpu_device, torch.bfloat16)
+    dbias = torch.full((N,), 0.5, device=gpu_device)
+    du, none = hip().gemm_fused(a, b, b_kn, 2, None, u, dbias)
+    assert none is None
+    uf = u.float().requires_grad_(True)
+    gelu_grad = torch.autograd.grad(torch.nn.functional.gelu(uf).sum(), uf)[0]
+    du_ref = (a.float() @ w.float().t()) * gelu_grad
+    _close(du, du_ref, 2e-2, 1e-2, "du")
+    # the bias gradient sums exactly the bf16 values written
+    _close(dbias, 0.5 + du.float().sum(0), 1e-3, 1e-4, "dbias")

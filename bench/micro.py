@@ -119,6 +119,26 @@ def fgemm(M: int = 65536) -> list[dict]:
     return rows
 
 
+def fgemm_one(K: int, N: int, epi: int = 0, b_kn: bool = False, M: int = 65536, reps: int = 20) -> None:
+    """Repeat one fused-GEMM launch (for rocprofv3 counter passes)."""
+    from llmtrain.ops import _ext
+
+    _ext.require()
+    ops = torch.ops.llmtrain_hip
+    dev = torch.device("cuda")
+    x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) / K**0.5
+    if b_kn:
+        w = w.t().contiguous()
+    bias = torch.randn(N, device=dev, dtype=torch.bfloat16)
+    u = torch.randn(M, N, device=dev, dtype=torch.bfloat16)
+    db = torch.zeros(N, device=dev)
+    fn = lambda: ops.gemm_fused(x, w, b_kn, epi, None if epi == 2 else bias, u if epi == 2 else None, db if epi == 2 else None)  # noqa: E731
+    ms = timeit(fn, iters=reps)
+    print(json.dumps({"K": K, "N": N, "epi": epi, "b_kn": b_kn, "ms": round(ms, 4),
+                      "TFLOPs": round(2.0 * M * K * N / ms / 1e9, 1)}), flush=True)
+
+
 def attn(B: int = 32, T: int = 1024, H: int = 12) -> list[dict]:
     from llmtrain.ops import _ext
 
@@ -157,6 +177,8 @@ if __name__ == "__main__":
         gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 65536, only="wgrad")
     if what == "fwd":  # forward / dX GEMMs
         gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 65536, only="fwd")
+    if what == "fgemm1":  # K N epi b_kn
+        fgemm_one(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5] == "1")
     if what == "fgemm":
         fgemm(int(sys.argv[2]) if len(sys.argv) > 2 else 65536)
     if what in ("attn", "all"):

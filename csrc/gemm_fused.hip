@@ -53,7 +53,8 @@ constexpr int kDmaB = kBElems * 2 / 1024 / 4;   // (4)
 constexpr int P = kDmaA + kDmaB;                // 8
 constexpr int kEpiFloats = 32 * 64;             // per-wave fp32 staging image [32][64]
 constexpr int kSmemElems = NSLOT * kSlotElems + 4 * kEpiFloats * 2;  // 160 KiB
-constexpr int kOob = 0x7ffffff0;                // buffer offset past any descriptor: dropped / 0
+constexpr int kOob = 0x7ffffff0;
+constexpr int kBand = 4;                        // n-tiles per raster band (see tile_origin)                // buffer offset past any descriptor: dropped / 0
 
 constexpr float kInvSqrt2 = 0.70710678118654752f;
 constexpr float kInvSqrt2Pi = 0.39894228040143268f;
@@ -117,6 +118,61 @@ __device__ __forceinline__ void dma4(unsigned lds_dst, int voff, __amdgpu_buffer
       : "memory");
 }
 
+// One stage of this wave's LDS-DMA: 4 A ops (1 KiB each, consecutive LDS KiB from dst_a) and 4 B
+// ops (from dst_b), one M0 save/restore per stage instead of per op.
+__device__ __forceinline__ void dma_stage(unsigned dst_a, unsigned dst_b, const int (&va)[4], const int (&vb)[4],
+                                          __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int soa, int sob) {
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %[keep], m0\n\t"
+      "s_mov_b32 m0, %[da]\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[a0], %[ra], %[soa] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[a1], %[ra], %[soa] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[a2], %[ra], %[soa] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[a3], %[ra], %[soa] offen lds\n\t"
+      "s_mov_b32 m0, %[db]\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[b0], %[rb], %[sob] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[b1], %[rb], %[sob] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[b2], %[rb], %[sob] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[b3], %[rb], %[sob] offen lds\n\t"
+      "s_mov_b32 m0, %[keep]"
+      : [keep] "=&s"(keep)
+      : [da] "s"(dst_a), [db] "s"(dst_b), [a0] "v"(va[0]), [a1] "v"(va[1]), [a2] "v"(va[2]), [a3] "v"(va[3]),
+        [b0] "v"(vb[0]), [b1] "v"(vb[1]), [b2] "v"(vb[2]), [b3] "v"(vb[3]), [ra] "s"(ra), [rb] "s"(rb),
+        [soa] "s"(soa), [sob] "s"(sob)
+      : "memory");
+}
+
+// Counted wait for a stage followed by the workgroup barrier: `later` stages (0/1) of P ops and,
+// when `post`, an epilogue's >= S VMEM ops were issued after it (in-order VM counter).
+template <int S>
+__device__ __forceinline__ void wait_one(bool later, bool post) {
+  constexpr int c11 = P + S > 63 ? 63 : P + S;
+  constexpr int c01 = S > 63 ? 63 : S;
+  if (later) {
+    if (post) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(c11) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(P) : "memory");
+  } else {
+    if (post) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(c01) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+}
+
 __device__ __forceinline__ bf16x8 lds_b128(const bf16_raw* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
 // element offset of (row, 16-byte chunk c) in a [rows][32] image swizzled by (row >> 2) & 3
@@ -132,7 +188,7 @@ struct Args {
   float* dbias;          // EPI 2: column sums (optional)
   int lda, ldb, ldc, ldu;
   int M, N, K;
-  int tiles_n, ntiles, nwg;
+  int tiles_m, tiles_n, ntiles, nwg;
 };
 
 template <bool NN, int EPI>
@@ -188,11 +244,26 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
 
   // issue cursor (stage stream over this workgroup's tiles)
   int is_s = 0, is_t = 0, is_m0 = 0, is_n0 = 0;
+  // Tile order: N is cut into bands of kBand tiles and the tiles run band-major, m-major inside
+  // a band.  The ~32 workgroups an XCD runs together then cover ~8 m-tiles x kBand n-tiles: the
+  // band's weight rows (kBand x 256 x K bf16, 1.5 MiB at K = 768) stay in that XCD's 4 MiB L2
+  // across rounds while activation strips stream through (m-major over all of N re-fetched the
+  // whole weight from the Infinity Cache every round).
   auto tile_origin = [&](int t, int& m0, int& n0) {
     const int w = base + jx + t * wgx;
-    const int mt = w / p.tiles_n;
+    const int full = p.tiles_n / kBand, per_band = p.tiles_m * kBand;
+    int mt, nt;
+    if (w < full * per_band) {
+      const int b = w / per_band, r = w - b * per_band;
+      mt = r / kBand;
+      nt = b * kBand + (r - mt * kBand);
+    } else {
+      const int wl = p.tiles_n - full * kBand, r = w - full * per_band;
+      mt = r / wl;
+      nt = full * kBand + (r - mt * wl);
+    }
     m0 = mt * BM;
-    n0 = (w - mt * p.tiles_n) * BN;
+    n0 = nt * BN;
   };
   tile_origin(0, is_m0, is_n0);
   auto issue = [&](int g) {
@@ -200,10 +271,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
     const int kk = is_s * BK;
     const int soa = (is_m0 * p.lda + kk) * 2;
     const int sob = NN ? (kk * p.ldb + is_n0) * 2 : (is_n0 * p.ldb + kk) * 2;
-#pragma unroll
-    for (int j = 0; j < kDmaA; ++j) dma16(slot + (wave * kDmaA + j) * 1024, va[j], ra, soa);
-#pragma unroll
-    for (int j = 0; j < kDmaB; ++j) dma16(slot + kAElems * 2 + (wave * kDmaB + j) * 1024, vb[j], rb, sob);
+    dma_stage(slot + wave * kDmaA * 1024, slot + kAElems * 2 + wave * kDmaB * 1024, va, vb, ra, rb, soa, sob);
     if (kBiasDma && is_s == nst - 1) {
       // the tile's bias (this wave's 128 columns, bf16) rides with its last K stage into the head
       // of the wave's epilogue staging image: landed by that stage's wait, read before staging
@@ -222,9 +290,30 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
   const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(EPI == 2 ? p.U : p.C), (short)0, p.M * (EPI == 2 ? p.ldu : p.ldc) * 2, 0x00020000);
 
+  // Software pipeline over the stage stream (NSLOT = 4 ring, stages g+2 and g+3 in flight while
+  // stage g computes).  Iteration g: read the second k16 half of stage g | MFMAs on the first
+  // half | wait stage g+1 + barrier | DMA stage g+3 into the slot stage g-1 vacated | read the
+  // first half of stage g+1 | MFMAs on the second half.  Every fragment read is issued one MFMA
+  // group before its use, and the barrier sits between MFMA groups.
+  auto read_frags = [&](int g, int ks, bf16x8 (&af)[4], bf16x8 (&bfr)[4]) {
+    const bf16_raw* aimg = smem + (g % NSLOT) * kSlotElems;
+    const bf16_raw* bimg = aimg + kAElems;
+    const int c = 2 * ks + (lane >> 5);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) af[b] = lds_b128(aimg + k32_off(wm * 128 + 32 * b + (lane & 31), c));
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      if (NN) bfr[a] = tr_frag<BN>(bimg, 16 * ks, wn * 128 + 32 * a, lane);
+      else bfr[a] = lds_b128(bimg + k32_off(wn * 128 + 32 * a + (lane & 31), c));
+    }
+  };
+
 #pragma unroll
   for (int g = 0; g < NSLOT - 1; ++g)
     if (g < total) issue(g);
+  wait_one<0>(total > 1, false);  // stage 0 landed (stage 1 and 2 may still fly: vmcnt(P) covers one)
+  bf16x8 af0[4], bf0[4], af1[4], bf1[4];
+  read_frags(0, 0, af0, bf0);
 
   int g = 0;  // global stage index of the stream
   for (int t = 0; t < my_tiles; ++t) {
@@ -235,28 +324,23 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
       for (int b = 0; b < 4; ++b) acc[a][b] = 0.f;
 
     for (int s = 0; s < nst; ++s, ++g) {
-      // the first NSLOT-1 waits of a tile after the first follow the previous tile's epilogue
-      wait_stage<EpiOps<EPI>::value>(min(total - 1 - g, NSLOT - 2), t > 0 && s < NSLOT - 1);
-      if (g + NSLOT - 1 < total) issue(g + NSLOT - 1);
-      const bf16_raw* aimg = smem + (g % NSLOT) * kSlotElems;
-      const bf16_raw* bimg = aimg + kAElems;
+      read_frags(g, 1, af1, bf1);
 #pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks) {
-        const int c = 2 * ks + (lane >> 5);
-        bf16x8 af[4], bfr[4];
+      for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) af[b] = lds_b128(aimg + k32_off(wm * 128 + 32 * b + (lane & 31), c));
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          if (NN) bfr[a] = tr_frag<BN>(bimg, 16 * ks, wn * 128 + 32 * a, lane);
-          else bfr[a] = lds_b128(bimg + k32_off(wn * 128 + 32 * a + (lane & 31), c));
-        }
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-          for (int b = 0; b < 4; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[a], af[b], acc[a][b], 0, 0, 0);
+        for (int b = 0; b < 4; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf0[a], af0[b], acc[a][b], 0, 0, 0);
+      if (g + 1 < total) {
+        // an epilogue ran after stage g+1 was issued iff one of the two previous stages ended a tile
+        wait_one<EpiOps<EPI>::value>(g + 2 < total, t > 0 && s < 2);
+        if (g + 3 < total) issue(g + 3);
+        read_frags(g + 1, 0, af0, bf0);
       }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf1[a], af1[b], acc[a][b], 0, 0, 0);
     }
 
     // ---------------- epilogue of tile t ----------------
@@ -414,7 +498,8 @@ hipError_t launch_gemm_fused(const GemmFusedArgs& g, hipStream_t stream) {
   a.N = g.N;
   a.K = g.K;
   a.tiles_n = (g.N + BN - 1) / BN;
-  a.ntiles = ((g.M + BM - 1) / BM) * a.tiles_n;
+  a.tiles_m = (g.M + BM - 1) / BM;
+  a.ntiles = a.tiles_m * a.tiles_n;
   const int ncu = gemm::cu_count();
   a.nwg = a.ntiles < ncu ? a.ntiles : ncu;
   switch (g.epilogue * 2 + (g.b_kn ? 1 : 0)) {

@@ -139,6 +139,29 @@ def fgemm_one(K: int, N: int, epi: int = 0, b_kn: bool = False, M: int = 65536, 
                       "TFLOPs": round(2.0 * M * K * N / ms / 1e9, 1)}), flush=True)
 
 
+def ln(M: int = 65536, d: int = 768) -> None:
+    """LayerNorm forward (+residual add) and backward at the engine's call shapes; GB/s moved."""
+    from llmtrain.ops import _ext
+
+    _ext.require()
+    ops = torch.ops.llmtrain_hip
+    dev = torch.device("cuda")
+    x = torch.randn(M, d, device=dev)
+    delta = torch.randn(M, d, device=dev, dtype=torch.bfloat16)
+    w = torch.ones(d, device=dev)
+    b = torch.zeros(d, device=dev)
+    xs, h, mu, rs = ops.add_layernorm_fwd(x, delta, w, b, 1e-5, torch.bfloat16)
+    ms = timeit(lambda: ops.add_layernorm_fwd(x, delta, w, b, 1e-5, torch.bfloat16))
+    gb = M * d * (4 + 2 + 4 + 2) / 1e9
+    print(json.dumps({"op": "add_ln_fwd", "ms": round(ms, 4), "GB/s": round(gb / ms * 1e3, 1)}), flush=True)
+    dy = torch.randn(M, d, device=dev, dtype=torch.bfloat16)
+    dres = torch.randn(M, d, device=dev)
+    dw, db, dp = (torch.zeros(d, device=dev) for _ in range(3))
+    ms = timeit(lambda: ops.layernorm_bwd(dy, xs, mu, rs, w, dres, dw, db, None, True, dp))
+    gb = M * d * (2 + 4 + 4 + 4 + 2) / 1e9
+    print(json.dumps({"op": "ln_bwd", "ms": round(ms, 4), "GB/s": round(gb / ms * 1e3, 1)}), flush=True)
+
+
 def attn(B: int = 32, T: int = 1024, H: int = 12) -> list[dict]:
     from llmtrain.ops import _ext
 
@@ -177,6 +200,8 @@ if __name__ == "__main__":
         gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 65536, only="wgrad")
     if what == "fwd":  # forward / dX GEMMs
         gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 65536, only="fwd")
+    if what == "ln":
+        ln()
     if what == "fgemm1":  # K N epi b_kn
         fgemm_one(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5] == "1")
     if what == "fgemm":

@@ -186,6 +186,9 @@ class FusedGPTEngine:
         # bandwidth-bound backward kernels of the main stream (LLMTRAIN_WGRAD_STREAM=0 disables)
         self.wgrad_stream_enabled = os.environ.get("LLMTRAIN_WGRAD_STREAM", "1") != "0"
         self._side: torch.cuda.Stream | None = None
+        # LM-head weight gradient on the side stream (LLMTRAIN_HEAD_WGRAD_SIDE=1; same-box A/B: no gain,
+        # the 5 ms GEMM and the block kernels it would overlap both want the whole chip)
+        self.head_wgrad_side = os.environ.get("LLMTRAIN_HEAD_WGRAD_SIDE", "0") == "1"
 
     # ------------------------------------------------------------------------------------
 
@@ -326,12 +329,22 @@ class FusedGPTEngine:
         assert dlogits is not None and st.hf is not None
         head = self.store.shadow_of(self.head_weight, padded=True)
 
-        # LM head: dhf = dlogits @ W ; dW += dlogits^T @ (go * hf).  Stays on the main stream: on
-        # the side stream, record_stream would pin the multi-GB dlogits block past the step and
-        # force fresh allocations every step (measured: 2.5x slower).
+        # LM head: dhf = dlogits @ W ; dW += dlogits^T @ (go * hf).  The weight gradient runs on
+        # the side stream, overlapping the last blocks' bandwidth-bound backward kernels.  No
+        # record_stream (it would pin the multi-GB dlogits block past the step and force fresh
+        # allocations every step): the engine holds dlogits until the main stream has joined the
+        # side stream at the end of the backward, so its memory is reused only after the GEMM.
         dhf = torch.mm(dlogits, head)
         hf_scaled = (st.hf.float() * go).to(st.hf.dtype) if st.hf.dtype != torch.float32 else st.hf * go
-        accumulate_wgrad(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled)
+        side = self._side_stream() if self.head_wgrad_side else None
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                accumulate_wgrad(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled)
+            held = (dlogits, hf_scaled)
+        else:
+            accumulate_wgrad(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled)
+            held = None
         del hf_scaled
         st.dlogits = None
         del dlogits
@@ -387,3 +400,4 @@ class FusedGPTEngine:
         )
         self._notify("embed")
         self._join_side()  # clip / optimizer / loss readers on the main stream see every gradient
+        del held  # the side stream's head GEMM is ordered before any reuse of these blocks

@@ -355,7 +355,7 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tens
   const int64_t M = a.size(0), K = a.size(1);
   const int64_t N = b_kn ? b.size(1) : b.size(0);
   TORCH_CHECK((b_kn ? b.size(0) : b.size(1)) == K, "gemm_fused: inner dimensions differ");
-  TORCH_CHECK(K % 32 == 0 && K >= 128 && N % 8 == 0, "gemm_fused: needs K % 32 == 0, K >= 128, N % 8 == 0");
+  TORCH_CHECK(K % 64 == 0 && K >= 256 && N % 8 == 0, "gemm_fused: needs K % 64 == 0, K >= 256, N % 8 == 0");
   TORCH_CHECK(epilogue >= 0 && epilogue <= 2, "gemm_fused: epilogue must be 0, 1 or 2");
   at::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
   llmt::GemmFusedArgs g;

@@ -44,17 +44,17 @@ using namespace gemm;
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 256, BN = 256, BK = 32, NSLOT = 4, kThreads = 256;
-constexpr int kAElems = BM * BK;                // [256][32]
-constexpr int kBElems = BN * BK;                // [256][32] or [32][256]
-constexpr int kSlotElems = kAElems + kBElems;   // 32 KiB
-constexpr int kDmaA = kAElems * 2 / 1024 / 4;   // 1-KiB DMA ops per wave per stage (4)
-constexpr int kDmaB = kBElems * 2 / 1024 / 4;   // (4)
-constexpr int P = kDmaA + kDmaB;                // 8
+constexpr int BM = 256, BN = 256, BK = 64, NSLOT = 2, kThreads = 256;
+constexpr int kAElems = BM * BK;                // [256][64]: 128-byte rows = whole cache lines
+constexpr int kBElems = BN * BK;                // [256][64] or [64][256]
+constexpr int kSlotElems = kAElems + kBElems;   // 64 KiB
+constexpr int kDmaA = kAElems * 2 / 1024 / 4;   // 1-KiB DMA ops per wave per stage (8)
+constexpr int kDmaB = kBElems * 2 / 1024 / 4;   // (8)
+constexpr int P = kDmaA + kDmaB;                // 16
 constexpr int kEpiFloats = 32 * 64;             // per-wave fp32 staging image [32][64]
 constexpr int kSmemElems = NSLOT * kSlotElems + 4 * kEpiFloats * 2;  // 160 KiB
-constexpr int kOob = 0x7ffffff0;
-constexpr int kBand = 4;                        // n-tiles per raster band (see tile_origin)                // buffer offset past any descriptor: dropped / 0
+constexpr int kOob = 0x7ffffff0;                // buffer offset past any descriptor: dropped / 0
+constexpr int kBand = 4;                        // n-tiles per raster band (see tile_origin)
 
 constexpr float kInvSqrt2 = 0.70710678118654752f;
 constexpr float kInvSqrt2Pi = 0.39894228040143268f;
@@ -86,23 +86,6 @@ struct EpiOps {
   static constexpr int value = EPI == 0 ? 32 : 64;
 };
 
-// Wait until the stage `n` stages before the newest issued one has landed, then barrier.
-// `post`: an epilogue's S VMEM ops were issued after the newest stage (in-order VM counter).
-template <int S>
-__device__ __forceinline__ void wait_stage(int n, bool post) {
-  constexpr int s2 = 2 * P + S > 63 ? 63 : 2 * P + S;
-  constexpr int s1 = P + S > 63 ? 63 : P + S;
-  if (n >= 2) {
-    if (post) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(s2) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * P) : "memory");
-  } else if (n == 1) {
-    if (post) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(s1) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(P) : "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  }
-}
-
 // one 256-byte LDS-DMA op (4 bytes per lane), M0 saved/restored like dma16
 __device__ __forceinline__ void dma4(unsigned lds_dst, int voff, __amdgpu_buffer_rsrc_t rsrc, int soff) {
   unsigned keep;
@@ -118,9 +101,9 @@ __device__ __forceinline__ void dma4(unsigned lds_dst, int voff, __amdgpu_buffer
       : "memory");
 }
 
-// One stage of this wave's LDS-DMA: 4 A ops (1 KiB each, consecutive LDS KiB from dst_a) and 4 B
+// One stage of this wave's LDS-DMA: 8 A ops (1 KiB each, consecutive LDS KiB from dst_a) and 8 B
 // ops (from dst_b), one M0 save/restore per stage instead of per op.
-__device__ __forceinline__ void dma_stage(unsigned dst_a, unsigned dst_b, const int (&va)[4], const int (&vb)[4],
+__device__ __forceinline__ void dma_stage(unsigned dst_a, unsigned dst_b, const int (&va)[8], const int (&vb)[8],
                                           __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int soa, int sob) {
   unsigned keep;
   asm volatile(
@@ -138,6 +121,18 @@ __device__ __forceinline__ void dma_stage(unsigned dst_a, unsigned dst_b, const 
       "s_add_u32 m0, m0, 0x400\n\t"
       "s_nop 0\n\t"
       "buffer_load_dwordx4 %[a3], %[ra], %[soa] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[a4], %[ra], %[soa] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[a5], %[ra], %[soa] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[a6], %[ra], %[soa] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[a7], %[ra], %[soa] offen lds\n\t"
       "s_mov_b32 m0, %[db]\n\t"
       "s_nop 0\n\t"
       "buffer_load_dwordx4 %[b0], %[rb], %[sob] offen lds\n\t"
@@ -150,33 +145,47 @@ __device__ __forceinline__ void dma_stage(unsigned dst_a, unsigned dst_b, const 
       "s_add_u32 m0, m0, 0x400\n\t"
       "s_nop 0\n\t"
       "buffer_load_dwordx4 %[b3], %[rb], %[sob] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[b4], %[rb], %[sob] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[b5], %[rb], %[sob] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[b6], %[rb], %[sob] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[b7], %[rb], %[sob] offen lds\n\t"
       "s_mov_b32 m0, %[keep]"
       : [keep] "=&s"(keep)
       : [da] "s"(dst_a), [db] "s"(dst_b), [a0] "v"(va[0]), [a1] "v"(va[1]), [a2] "v"(va[2]), [a3] "v"(va[3]),
-        [b0] "v"(vb[0]), [b1] "v"(vb[1]), [b2] "v"(vb[2]), [b3] "v"(vb[3]), [ra] "s"(ra), [rb] "s"(rb),
-        [soa] "s"(soa), [sob] "s"(sob)
+        [a4] "v"(va[4]), [a5] "v"(va[5]), [a6] "v"(va[6]), [a7] "v"(va[7]), [b0] "v"(vb[0]), [b1] "v"(vb[1]),
+        [b2] "v"(vb[2]), [b3] "v"(vb[3]), [b4] "v"(vb[4]), [b5] "v"(vb[5]), [b6] "v"(vb[6]), [b7] "v"(vb[7]),
+        [ra] "s"(ra), [rb] "s"(rb), [soa] "s"(soa), [sob] "s"(sob)
       : "memory");
 }
 
-// Counted wait for a stage followed by the workgroup barrier: `later` stages (0/1) of P ops and,
-// when `post`, an epilogue's >= S VMEM ops were issued after it (in-order VM counter).
+// Wait for the newest issued stage (nothing was issued after it but, when `post`, an epilogue's
+// >= S VMEM ops; in-order VM counter), retire this wave's LDS reads, then the workgroup barrier:
+// afterwards the stage is visible to every wave and the other ring slot is free to refill.
 template <int S>
-__device__ __forceinline__ void wait_one(bool later, bool post) {
-  constexpr int c11 = P + S > 63 ? 63 : P + S;
-  constexpr int c01 = S > 63 ? 63 : S;
-  if (later) {
-    if (post) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(c11) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(P) : "memory");
-  } else {
-    if (post) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(c01) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  }
+__device__ __forceinline__ void wait_ring(bool post) {
+  constexpr int cs = S > 63 ? 63 : S;
+  if (post) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(cs) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 __device__ __forceinline__ bf16x8 lds_b128(const bf16_raw* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
-// element offset of (row, 16-byte chunk c) in a [rows][32] image swizzled by (row >> 2) & 3
-__device__ __forceinline__ int k32_off(int row, int c) { return row * 32 + 8 * (c ^ ((row >> 2) & 3)); }
+// element offset of (row, 16-byte chunk c) in a [rows][64] image (128-byte rows) with the chunk
+// XOR-swizzled by G(row) = g((row >> 1) & 7), g(k) = ((k & 1) << 2) | (k >> 1): the 16 rows of a
+// ds_read_b128 lane group are distinct mod 16, and G spreads them over all 16 bank slots
+__device__ __forceinline__ int swz_g(int row) {
+  const int k = (row >> 1) & 7;
+  return ((k & 1) << 2) | (k >> 1);
+}
+__device__ __forceinline__ int k64_off(int row, int c) { return row * 64 + 8 * (c ^ swz_g(row)); }
 
 struct Args {
   const bf16_raw* A;
@@ -217,21 +226,19 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
   // per-lane DMA source offsets (bytes, relative to the stage's scalar offset)
   int va[kDmaA], vb[kDmaB];
 #pragma unroll
-  for (int j = 0; j < kDmaA; ++j) {  // A image: 16 rows of 64 B per op
-    const int row = (wave * kDmaA + j) * 16 + (lane >> 2);
-    const int c = (lane & 3) ^ ((row >> 2) & 3);
-    va[j] = (row * p.lda + 8 * c) * 2;
+  for (int j = 0; j < kDmaA; ++j) {  // A image: 8 rows of 128 B per op
+    const int row = (wave * kDmaA + j) * 8 + (lane >> 3);
+    va[j] = (row * p.lda + 8 * ((lane & 7) ^ swz_g(row))) * 2;
   }
 #pragma unroll
   for (int j = 0; j < kDmaB; ++j) {
-    if (NN) {  // [32 k][256 n]: 2 rows of 512 B per op, wgrad swizzle
+    if (NN) {  // [64 k][256 n]: 2 rows of 512 B per op, wgrad swizzle
       const int row = (wave * kDmaB + j) * 2 + (lane >> 5);
       const int c = (lane & 31) ^ ((row & 3) << 2);
       vb[j] = (row * p.ldb + 8 * c) * 2;
     } else {
-      const int row = (wave * kDmaB + j) * 16 + (lane >> 2);
-      const int c = (lane & 3) ^ ((row >> 2) & 3);
-      vb[j] = (row * p.ldb + 8 * c) * 2;
+      const int row = (wave * kDmaB + j) * 8 + (lane >> 3);
+      vb[j] = (row * p.ldb + 8 * ((lane & 7) ^ swz_g(row))) * 2;
     }
   }
   const unsigned lds_base = (unsigned)(unsigned long)(lds_void*)smem;
@@ -290,28 +297,37 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
   const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(EPI == 2 ? p.U : p.C), (short)0, p.M * (EPI == 2 ? p.ldu : p.ldc) * 2, 0x00020000);
 
-  // Software pipeline over the stage stream (NSLOT = 4 ring, stages g+2 and g+3 in flight while
-  // stage g computes).  Iteration g: read the second k16 half of stage g | MFMAs on the first
-  // half | wait stage g+1 + barrier | DMA stage g+3 into the slot stage g-1 vacated | read the
-  // first half of stage g+1 | MFMAs on the second half.  Every fragment read is issued one MFMA
-  // group before its use, and the barrier sits between MFMA groups.
+  // Software pipeline over the stage stream (2-slot ring of 64-deep stages; stage g+1 lands while
+  // stage g computes).  Iteration g runs its four k16 MFMA groups with every fragment read issued
+  // one group ahead; before the last group: wait stage g+1 + retire reads + barrier, DMA stage g+2
+  // into the slot stage g vacated, read the first fragments of stage g+1.
   auto read_frags = [&](int g, int ks, bf16x8 (&af)[4], bf16x8 (&bfr)[4]) {
     const bf16_raw* aimg = smem + (g % NSLOT) * kSlotElems;
     const bf16_raw* bimg = aimg + kAElems;
     const int c = 2 * ks + (lane >> 5);
 #pragma unroll
-    for (int b = 0; b < 4; ++b) af[b] = lds_b128(aimg + k32_off(wm * 128 + 32 * b + (lane & 31), c));
+    for (int b = 0; b < 4; ++b) af[b] = lds_b128(aimg + k64_off(wm * 128 + 32 * b + (lane & 31), c));
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       if (NN) bfr[a] = tr_frag<BN>(bimg, 16 * ks, wn * 128 + 32 * a, lane);
-      else bfr[a] = lds_b128(bimg + k32_off(wn * 128 + 32 * a + (lane & 31), c));
+      else bfr[a] = lds_b128(bimg + k64_off(wn * 128 + 32 * a + (lane & 31), c));
     }
   };
-
+  auto mfma_group = [&](f32x16 (&acc)[4][4], const bf16x8 (&af)[4], const bf16x8 (&bfr)[4]) {
 #pragma unroll
-  for (int g = 0; g < NSLOT - 1; ++g)
-    if (g < total) issue(g);
-  wait_one<0>(total > 1, false);  // stage 0 landed (stage 1 and 2 may still fly: vmcnt(P) covers one)
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[a], af[b], acc[a][b], 0, 0, 0);
+  };
+
+  issue(0);
+  if (total > 1) {
+    issue(1);
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(P) : "memory");  // stage 0 (stage 1 flies)
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
   bf16x8 af0[4], bf0[4], af1[4], bf1[4];
   read_frags(0, 0, af0, bf0);
 
@@ -325,22 +341,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
 
     for (int s = 0; s < nst; ++s, ++g) {
       read_frags(g, 1, af1, bf1);
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf0[a], af0[b], acc[a][b], 0, 0, 0);
+      mfma_group(acc, af0, bf0);
+      read_frags(g, 2, af0, bf0);
+      mfma_group(acc, af1, bf1);
+      read_frags(g, 3, af1, bf1);
+      mfma_group(acc, af0, bf0);
       if (g + 1 < total) {
-        // an epilogue ran after stage g+1 was issued iff one of the two previous stages ended a tile
-        wait_one<EpiOps<EPI>::value>(g + 2 < total, t > 0 && s < 2);
-        if (g + 3 < total) issue(g + 3);
+        // stage g+1 was issued last, in iteration g-1; an epilogue after it iff g starts a tile
+        wait_ring<EpiOps<EPI>::value>(t > 0 && s == 0);
+        if (g + 2 < total) issue(g + 2);
         read_frags(g + 1, 0, af0, bf0);
       }
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf1[a], af1[b], acc[a][b], 0, 0, 0);
+      mfma_group(acc, af1, bf1);
     }
 
     // ---------------- epilogue of tile t ----------------

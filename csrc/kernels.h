@@ -108,7 +108,7 @@ hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, fl
 // C[M, N] = epi(A[M, K] . op(B)); B is [N, ldb] (K contiguous, b_kn = false) or [K, ldb]
 // (N contiguous, b_kn = true).  epilogue 0: C = acc + bias (bias optional);
 // 1: C = acc + bias (pre-activation), c2 = gelu(C); 2: C = acc * gelu'(u), dbias += colsum(C).
-// c2 shares C's leading dimension.  K % 32 == 0, K >= 128, N % 8 == 0, leading dimensions % 8 == 0.
+// c2 shares C's leading dimension.  K % 64 == 0, K >= 256, N % 8 == 0, leading dimensions % 8 == 0.
 struct GemmFusedArgs {
   const void* a = nullptr;
   int lda = 0;

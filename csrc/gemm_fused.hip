@@ -198,6 +198,7 @@ struct Args {
   int lda, ldb, ldc, ldu;
   int M, N, K;
   int tiles_m, tiles_n, ntiles, nwg;
+  int debug;
 };
 
 template <bool NN, int EPI>
@@ -278,7 +279,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
     const int kk = is_s * BK;
     const int soa = (is_m0 * p.lda + kk) * 2;
     const int sob = NN ? (kk * p.ldb + is_n0) * 2 : (is_n0 * p.ldb + kk) * 2;
-    dma_stage(slot + wave * kDmaA * 1024, slot + kAElems * 2 + wave * kDmaB * 1024, va, vb, ra, rb, soa, sob);
+    if (!(p.debug & 1))  // debug bit 0: skip the operand DMA (times the compute skeleton alone)
+      dma_stage(slot + wave * kDmaA * 1024, slot + kAElems * 2 + wave * kDmaB * 1024, va, vb, ra, rb, soa, sob);
     if (kBiasDma && is_s == nst - 1) {
       // the tile's bias (this wave's 128 columns, bf16) rides with its last K stage into the head
       // of the wave's epilogue staging image: landed by that stage's wait, read before staging
@@ -514,6 +516,11 @@ hipError_t launch_gemm_fused(const GemmFusedArgs& g, hipStream_t stream) {
   a.ntiles = a.tiles_m * a.tiles_n;
   const int ncu = gemm::cu_count();
   a.nwg = a.ntiles < ncu ? a.ntiles : ncu;
+  static const int debug = [] {
+    const char* e = std::getenv("LLMT_FGEMM_DEBUG");
+    return e ? std::atoi(e) : 0;
+  }();
+  a.debug = debug;
   switch (g.epilogue * 2 + (g.b_kn ? 1 : 0)) {
     case 0: launch_one<false, 0>(a, stream); break;
     case 1: launch_one<true, 0>(a, stream); break;

@@ -74,7 +74,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", choices=sorted(MODELS), default="gpt2-124m")
-    ap.add_argument("--micro-batch", type=int, default=64, help="sequences per GPU per micro-step")
+    ap.add_argument("--micro-batch", type=int, default=128, help="sequences per GPU per micro-step")
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--path", choices=["fused", "module"], default="fused")
@@ -155,6 +155,10 @@ def main() -> int:
             "mfu": round(mfu(tps / world, per_tok), 4),
             "final_loss": round(final_loss, 4),
             "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 2),
+            "alloc_retries": int(torch.cuda.memory_stats().get("num_alloc_retries", 0)),
+            "device_mallocs": int(torch.cuda.memory_stats().get("num_device_alloc", 0)),
+            "reserved_gib": round(torch.cuda.memory_reserved() / 2**30, 2),
+            "device_free_total_gib": [round(v / 2**30, 1) for v in torch.cuda.mem_get_info()],
         }
         print(json.dumps(result), flush=True)
     if ddp_state is not None:

@@ -218,7 +218,13 @@ hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, fl
     }();
     tile = forced;
   }
-  const int ncu = gemm::cu_count();
+  // LLMT_WGRAD_CUS: plan the split for fewer CUs than the chip has, leaving room for the main
+  // stream's kernels when the weight gradients run on the side stream (A/B knob)
+  static const int cus_env = [] {
+    const char* e = std::getenv("LLMT_WGRAD_CUS");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int ncu = cus_env > 0 ? cus_env : gemm::cu_count();
   wgrad::Plan p;
   if (tile == 128 || tile == 256) {
     p = wgrad::plan_for(tile, M, N, K, split, ncu);

@@ -43,16 +43,18 @@ namespace fgemm {
 using namespace gemm;
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int BM = 256, BN = 256, BK = 64, NSLOT = 2, kThreads = 256;
+constexpr int BM = 256, BN = 256, BK = 64, NSLOT = 2;
+constexpr int kWaves = 8, kThreads = 64 * kWaves;  // two waves per SIMD
 constexpr int kAElems = BM * BK;                // [256][64]: 128-byte rows = whole cache lines
 constexpr int kBElems = BN * BK;                // [256][64] or [64][256]
 constexpr int kSlotElems = kAElems + kBElems;   // 64 KiB
-constexpr int kDmaA = kAElems * 2 / 1024 / 4;   // 1-KiB DMA ops per wave per stage (8)
-constexpr int kDmaB = kBElems * 2 / 1024 / 4;   // (8)
-constexpr int P = kDmaA + kDmaB;                // 16
-constexpr int kEpiFloats = 32 * 64;             // per-wave fp32 staging image [32][64]
-constexpr int kSmemElems = NSLOT * kSlotElems + 4 * kEpiFloats * 2;  // 160 KiB
+constexpr int kDmaA = kAElems * 2 / 1024 / kWaves;  // 1-KiB DMA ops per wave per stage (4)
+constexpr int kDmaB = kBElems * 2 / 1024 / kWaves;  // (4)
+constexpr int P = kDmaA + kDmaB;                // 8
+constexpr int kEpiFloats = 32 * 32;             // per-wave fp32 staging image [32][32] (4 KiB)
+constexpr int kSmemElems = NSLOT * kSlotElems + kWaves * kEpiFloats * 2;  // 160 KiB
 constexpr int kOob = 0x7ffffff0;                // buffer offset past any descriptor: dropped / 0
 constexpr int kBand = 4;                        // n-tiles per raster band (see tile_origin)
 
@@ -101,9 +103,9 @@ __device__ __forceinline__ void dma4(unsigned lds_dst, int voff, __amdgpu_buffer
       : "memory");
 }
 
-// One stage of this wave's LDS-DMA: 8 A ops (1 KiB each, consecutive LDS KiB from dst_a) and 8 B
+// One stage of this wave's LDS-DMA: 4 A ops (1 KiB each, consecutive LDS KiB from dst_a) and 4 B
 // ops (from dst_b), one M0 save/restore per stage instead of per op.
-__device__ __forceinline__ void dma_stage(unsigned dst_a, unsigned dst_b, const int (&va)[8], const int (&vb)[8],
+__device__ __forceinline__ void dma_stage(unsigned dst_a, unsigned dst_b, const int (&va)[4], const int (&vb)[4],
                                           __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int soa, int sob) {
   unsigned keep;
   asm volatile(
@@ -121,18 +123,6 @@ __device__ __forceinline__ void dma_stage(unsigned dst_a, unsigned dst_b, const 
       "s_add_u32 m0, m0, 0x400\n\t"
       "s_nop 0\n\t"
       "buffer_load_dwordx4 %[a3], %[ra], %[soa] offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %[a4], %[ra], %[soa] offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %[a5], %[ra], %[soa] offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %[a6], %[ra], %[soa] offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %[a7], %[ra], %[soa] offen lds\n\t"
       "s_mov_b32 m0, %[db]\n\t"
       "s_nop 0\n\t"
       "buffer_load_dwordx4 %[b0], %[rb], %[sob] offen lds\n\t"
@@ -145,24 +135,11 @@ __device__ __forceinline__ void dma_stage(unsigned dst_a, unsigned dst_b, const 
       "s_add_u32 m0, m0, 0x400\n\t"
       "s_nop 0\n\t"
       "buffer_load_dwordx4 %[b3], %[rb], %[sob] offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %[b4], %[rb], %[sob] offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %[b5], %[rb], %[sob] offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %[b6], %[rb], %[sob] offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %[b7], %[rb], %[sob] offen lds\n\t"
       "s_mov_b32 m0, %[keep]"
       : [keep] "=&s"(keep)
       : [da] "s"(dst_a), [db] "s"(dst_b), [a0] "v"(va[0]), [a1] "v"(va[1]), [a2] "v"(va[2]), [a3] "v"(va[3]),
-        [a4] "v"(va[4]), [a5] "v"(va[5]), [a6] "v"(va[6]), [a7] "v"(va[7]), [b0] "v"(vb[0]), [b1] "v"(vb[1]),
-        [b2] "v"(vb[2]), [b3] "v"(vb[3]), [b4] "v"(vb[4]), [b5] "v"(vb[5]), [b6] "v"(vb[6]), [b7] "v"(vb[7]),
-        [ra] "s"(ra), [rb] "s"(rb), [soa] "s"(soa), [sob] "s"(sob)
+        [b0] "v"(vb[0]), [b1] "v"(vb[1]), [b2] "v"(vb[2]), [b3] "v"(vb[3]), [ra] "s"(ra), [rb] "s"(rb),
+        [soa] "s"(soa), [sob] "s"(sob)
       : "memory");
 }
 
@@ -206,7 +183,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
   __shared__ __attribute__((aligned(16))) bf16_raw smem[kSmemElems];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  // two wave groups (waves 0-3 / 4-7: one wave of each per SIMD) own the upper / lower 128 rows
+  // of the tile; wave wq of a group owns 64 columns -> a 128x64 wave tile (4 x 2 MFMA tiles)
+  const int wm = wave >> 2, wn = wave & 3;
 
   // ---- this workgroup's tiles: XCD-contiguous range, strided by the XCD's workgroup count
   const int L = blockIdx.x, xcd = L & 7, jx = L >> 3;
@@ -284,7 +263,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
     if (kBiasDma && is_s == nst - 1) {
       // the tile's bias (this wave's 128 columns, bf16) rides with its last K stage into the head
       // of the wave's epilogue staging image: landed by that stage's wait, read before staging
-      dma4(epi_lds, lane * 4, rbias, (is_n0 + wn * 128) * 2);
+      dma4(epi_lds, lane * 4, rbias, (is_n0 + wn * 64) * 2);
     }
     if (++is_s == nst) {
       is_s = 0;
@@ -303,21 +282,21 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
   // stage g computes).  Iteration g runs its four k16 MFMA groups with every fragment read issued
   // one group ahead; before the last group: wait stage g+1 + retire reads + barrier, DMA stage g+2
   // into the slot stage g vacated, read the first fragments of stage g+1.
-  auto read_frags = [&](int g, int ks, bf16x8 (&af)[4], bf16x8 (&bfr)[4]) {
+  auto read_frags = [&](int g, int ks, bf16x8 (&af)[4], bf16x8 (&bfr)[2]) {
     const bf16_raw* aimg = smem + (g % NSLOT) * kSlotElems;
     const bf16_raw* bimg = aimg + kAElems;
     const int c = 2 * ks + (lane >> 5);
 #pragma unroll
     for (int b = 0; b < 4; ++b) af[b] = lds_b128(aimg + k64_off(wm * 128 + 32 * b + (lane & 31), c));
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      if (NN) bfr[a] = tr_frag<BN>(bimg, 16 * ks, wn * 128 + 32 * a, lane);
-      else bfr[a] = lds_b128(bimg + k64_off(wn * 128 + 32 * a + (lane & 31), c));
+    for (int a = 0; a < 2; ++a) {
+      if (NN) bfr[a] = tr_frag<BN>(bimg, 16 * ks, wn * 64 + 32 * a, lane);
+      else bfr[a] = lds_b128(bimg + k64_off(wn * 64 + 32 * a + (lane & 31), c));
     }
   };
-  auto mfma_group = [&](f32x16 (&acc)[4][4], const bf16x8 (&af)[4], const bf16x8 (&bfr)[4]) {
+  auto mfma_group = [&](f32x16 (&acc)[2][4], const bf16x8 (&af)[4], const bf16x8 (&bfr)[2]) {
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b)
         acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[a], af[b], acc[a][b], 0, 0, 0);
@@ -330,14 +309,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
   } else {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
-  bf16x8 af0[4], bf0[4], af1[4], bf1[4];
+  bf16x8 af0[4], bf0[2], af1[4], bf1[2];
   read_frags(0, 0, af0, bf0);
 
   int g = 0;  // global stage index of the stream
   for (int t = 0; t < my_tiles; ++t) {
-    f32x16 acc[4][4];  // [n-tile a][m-tile b]
+    f32x16 acc[2][4];  // [n-tile a][m-tile b]
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) acc[a][b] = 0.f;
 
@@ -358,95 +337,89 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
     }
 
     // ---------------- epilogue of tile t ----------------
+    // per 32x32 accumulator tile: registers -> [32 m][32 n] fp32 LDS image (16-byte chunks XOR
+    // (row & 7)) -> 8 rows x 4 columns per lane-octet read back -> 8-byte row segments
     int m0, n0;
     tile_origin(t, m0, n0);
-    const int mw = m0 + wm * 128, nw = n0 + wn * 128;
-    const int q8 = lane & 7;  // this lane's 8-column group within a 64-column half
-    float bias_f[2][8];
-    float csum[2][8];
+    const int mw = m0 + wm * 128, nw = n0 + wn * 64;
+    const int q = lane & 7;  // this lane's 4-column group within a 32-column tile
+    float bias_f[2][4];
+    float csum[2][4];
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        bias_f[h][k] = 0.f;
-        csum[h][k] = 0.f;
+      for (int k = 0; k < 4; ++k) {
+        bias_f[a][k] = 0.f;
+        csum[a][k] = 0.f;
       }
     if (kBiasDma) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const ushort8_t bv = *reinterpret_cast<const ushort8_t*>(reinterpret_cast<const bf16_raw*>(epi) + 64 * h + 8 * q8);
+      for (int a = 0; a < 2; ++a) {
+        const ushort4_t bv = *reinterpret_cast<const ushort4_t*>(reinterpret_cast<const bf16_raw*>(epi) + 32 * a + 4 * q);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) bias_f[h][k] = bf2f(bv[k]);
+        for (int k = 0; k < 4; ++k) bias_f[a][k] = bf2f(bv[k]);
       }
     }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int a = 0; a < 2; ++a) {
         __builtin_amdgcn_sched_barrier(0);
-        // registers -> LDS image [32 m][64 n] fp32, 16-byte chunk index XOR (row & 7)
         const int row = lane & 31;
 #pragma unroll
-        for (int a2 = 0; a2 < 2; ++a2) {
-#pragma unroll
-          for (int gq = 0; gq < 4; ++gq) {
-            const int ch = 8 * a2 + 2 * gq + (lane >> 5);
-            const f32x16& v = acc[2 * h + a2][b];
-            *reinterpret_cast<float4_t*>(epi + row * 64 + 4 * (ch ^ (row & 7))) =
-                float4_t{v[4 * gq], v[4 * gq + 1], v[4 * gq + 2], v[4 * gq + 3]};
-          }
+        for (int gq = 0; gq < 4; ++gq) {
+          const int ch = 2 * gq + (lane >> 5);
+          const f32x16& v = acc[a][b];
+          *reinterpret_cast<float4_t*>(epi + row * 32 + 4 * (ch ^ (row & 7))) =
+              float4_t{v[4 * gq], v[4 * gq + 1], v[4 * gq + 2], v[4 * gq + 3]};
         }
         __builtin_amdgcn_sched_barrier(0);  // wave-local: LDS executes a wave's ops in order
-        float vals[4][8];
+        float4_t vals[4];
         int off[4];
 #pragma unroll
         for (int it = 0; it < 4; ++it) {
           const int R = 8 * it + (lane >> 3);
-          const float4_t lo = *reinterpret_cast<const float4_t*>(epi + R * 64 + 4 * ((2 * q8) ^ (R & 7)));
-          const float4_t hi = *reinterpret_cast<const float4_t*>(epi + R * 64 + 4 * ((2 * q8 + 1) ^ (R & 7)));
-          vals[it][0] = lo[0]; vals[it][1] = lo[1]; vals[it][2] = lo[2]; vals[it][3] = lo[3];
-          vals[it][4] = hi[0]; vals[it][5] = hi[1]; vals[it][6] = hi[2]; vals[it][7] = hi[3];
-          const int m = mw + 32 * b + R, n = nw + 64 * h + 8 * q8;
+          vals[it] = *reinterpret_cast<const float4_t*>(epi + R * 32 + 4 * (q ^ (R & 7)));
+          const int m = mw + 32 * b + R, n = nw + 32 * a + 4 * q;
           off[it] = (m < p.M && n < p.N) ? (m * p.ldc + n) * 2 : kOob;
         }
         asm volatile("" ::: "memory");
         if (EPI == 2) {
-          u32x4 uraw[4];
+          u32x2 uraw[4];
 #pragma unroll
           for (int it = 0; it < 4; ++it) {
             const int R = 8 * it + (lane >> 3);
-            const int m = mw + 32 * b + R, n = nw + 64 * h + 8 * q8;
+            const int m = mw + 32 * b + R, n = nw + 32 * a + 4 * q;
             const int uoff = (m < p.M && n < p.N) ? (m * p.ldu + n) * 2 : kOob;
-            uraw[it] = __builtin_amdgcn_raw_buffer_load_b128(ru, uoff, 0, 0);
+            uraw[it] = __builtin_amdgcn_raw_buffer_load_b64(ru, uoff, 0, 0);
           }
 #pragma unroll
           for (int it = 0; it < 4; ++it) {
-            __builtin_amdgcn_sched_barrier(0);  // one row of 8 at a time: bounded VGPR pressure
-            const ushort8_t uv = __builtin_bit_cast(ushort8_t, uraw[it]);
-            float o[8];
+            __builtin_amdgcn_sched_barrier(0);  // one row segment at a time: bounded VGPR pressure
+            const ushort4_t uv = __builtin_bit_cast(ushort4_t, uraw[it]);
+            ushort4_t ov;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              o[k] = bf2f(f2bf(vals[it][k] * gelu_grad(bf2f(uv[k]))));
-              csum[h][k] += o[k];
+            for (int k = 0; k < 4; ++k) {
+              ov[k] = f2bf(vals[it][k] * gelu_grad(bf2f(uv[k])));
+              csum[a][k] += bf2f(ov[k]);
             }
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(o)), rc, off[it], 0, 0);
-            // pin the running sums here: left alone, hipcc sinks all 128 adds to the end of the
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, ov), rc, off[it], 0, 0);
+            // pin the running sums here: left alone, hipcc sinks all the adds to the end of the
             // epilogue and keeps every product live (spills)
-            asm volatile("" : "+v"(csum[h][0]), "+v"(csum[h][1]), "+v"(csum[h][2]), "+v"(csum[h][3]),
-                         "+v"(csum[h][4]), "+v"(csum[h][5]), "+v"(csum[h][6]), "+v"(csum[h][7]));
+            asm volatile("" : "+v"(csum[a][0]), "+v"(csum[a][1]), "+v"(csum[a][2]), "+v"(csum[a][3]));
           }
         } else {
 #pragma unroll
           for (int it = 0; it < 4; ++it) {
-            float o[8];
+            ushort4_t ov;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) o[k] = vals[it][k] + bias_f[h][k];
-            const ushort8_t ov = pack8(o);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ov), rc, off[it], 0, 0);
+            for (int k = 0; k < 4; ++k) ov[k] = f2bf(vals[it][k] + bias_f[a][k]);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, ov), rc, off[it], 0, 0);
             if (EPI == 1) {
+              ushort4_t gv;
 #pragma unroll
-              for (int k = 0; k < 8; ++k) o[k] = gelu(bf2f(ov[k]));
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(o)), rc2, off[it], 0, 0);
+              for (int k = 0; k < 4; ++k) gv[k] = f2bf(gelu(bf2f(ov[k])));
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, gv), rc2, off[it], 0, 0);
             }
           }
         }
@@ -454,22 +427,22 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
     }
     if (EPI == 2 && p.dbias != nullptr) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+      for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          float s = csum[h][k];
-          s += __shfl_xor(s, 8, 64);
-          s += __shfl_xor(s, 16, 64);
-          s += __shfl_xor(s, 32, 64);
-          csum[h][k] = s;
+        for (int k = 0; k < 4; ++k) {
+          float v = csum[a][k];
+          v += __shfl_xor(v, 8, 64);
+          v += __shfl_xor(v, 16, 64);
+          v += __shfl_xor(v, 32, 64);
+          csum[a][k] = v;
         }
       if (lane < 8) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int n = nw + 64 * h + 8 * q8;
+        for (int a = 0; a < 2; ++a) {
+          const int n = nw + 32 * a + 4 * q;
           if (n < p.N) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) atomicAdd(p.dbias + n + k, csum[h][k]);
+            for (int k = 0; k < 4; ++k) atomicAdd(p.dbias + n + k, csum[a][k]);
           }
         }
       }

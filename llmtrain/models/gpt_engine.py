@@ -187,6 +187,10 @@ class FusedGPTEngine:
         # weight-gradient GEMMs on a second HIP stream, overlapping the dX GEMMs and the
         # bandwidth-bound backward kernels of the main stream (LLMTRAIN_WGRAD_STREAM=0 disables)
         self.wgrad_stream_enabled = os.environ.get("LLMTRAIN_WGRAD_STREAM", "1") != "0"
+        # hand-written MFMA GEMM (csrc/gemm_fused.hip) where it beats hipBLASLt: the MLP projection's
+        # dX with the GELU backward + fc-bias gradient in its epilogue, and the attention output
+        # projection forward/dX (LLMTRAIN_FUSED_GEMM=0: hipBLASLt + separate GELU backward)
+        self.fused_gemm = os.environ.get("LLMTRAIN_FUSED_GEMM", "1") != "0"
         self._side: torch.cuda.Stream | None = None
         self._pending: list[torch.Tensor] = []  # operands of side-stream GEMMs of the current block
         self._held: list[tuple[Any, list[torch.Tensor]]] = []  # (side event, operands) per block
@@ -265,11 +269,12 @@ class FusedGPTEngine:
         self._held.clear()
         self._pending = []
 
-    def _linear(self, x: torch.Tensor, layer: torch.nn.Linear) -> torch.Tensor:
+    def _linear(self, x: torch.Tensor, layer: torch.nn.Linear, *, fused: bool = False) -> torch.Tensor:
         w = self._w(layer.weight)
-        if layer.bias is None:
-            return torch.mm(x, w.t())
-        return torch.addmm(self._w(layer.bias), x, w.t())
+        b = None if layer.bias is None else self._w(layer.bias)
+        if fused and self.fused_gemm:
+            return ops.linear_fwd(x, w, b)
+        return torch.mm(x, w.t()) if b is None else torch.addmm(b, x, w.t())
 
     def loss(self, ids: torch.Tensor, labels: torch.Tensor, mask: torch.Tensor | None) -> torch.Tensor:
         self.store.sync_shadow()
@@ -308,7 +313,7 @@ class FusedGPTEngine:
             )  # site 3i = the previous block's MLP branch (unused for block 0: delta is None)
             qkv = self._linear(h1, blk.attn.qkv_proj)
             att, lse = ops.attn_fwd(qkv, bsz, seqlen, self.n_heads, dropout=state.site(2 + 3 * i))
-            y = self._linear(att, blk.attn.out_proj)
+            y = self._linear(att, blk.attn.out_proj, fused=True)
             xm, h2, mu2, rs2 = ops.add_layernorm_fwd(
                 xs, y, blk.ln_2.weight, blk.ln_2.bias, self.eps, cdt, dropout=state.site(1 + 3 * i)
             )
@@ -388,9 +393,12 @@ class FusedGPTEngine:
             blk, a = self.blocks[i], st.blocks[i]
             # MLP: delta = g Wp^T + bp ; dx is d(delta) (bias grad already summed by the LN bwd)
             self._wgrad(self._g(blk.mlp_proj.weight), dx_lp, a.g)
-            dg = torch.mm(dx_lp, self._w(blk.mlp_proj.weight))
-            du = ops.gelu_bwd(dg, a.u, self._g(blk.mlp_fc.bias))
-            del dg
+            if self.fused_gemm:  # GELU backward + fc bias grad in the dX GEMM's epilogue
+                du = ops.linear_dx_gelu_bwd(dx_lp, self._w(blk.mlp_proj.weight), a.u, self._g(blk.mlp_fc.bias))
+            else:
+                dg = torch.mm(dx_lp, self._w(blk.mlp_proj.weight))
+                du = ops.gelu_bwd(dg, a.u, self._g(blk.mlp_fc.bias))
+                del dg
             self._wgrad(self._g(blk.mlp_fc.weight), du, a.h2)
             dh2 = torch.mm(du, self._w(blk.mlp_fc.weight))
             del du
@@ -401,7 +409,8 @@ class FusedGPTEngine:
             del dh2, dx, dx_lp
             # attention output projection
             self._wgrad(self._g(blk.attn.out_proj.weight), dy_lp, a.att)
-            datt = torch.mm(dy_lp, self._w(blk.attn.out_proj.weight))
+            wo = self._w(blk.attn.out_proj.weight)
+            datt = ops.linear_dx(dy_lp, wo) if self.fused_gemm else torch.mm(dy_lp, wo)
             del dy_lp
             # the qkv-bias gradient (column sums of dqkv) is fused into the attention backward
             dqkv = ops.attn_bwd(

@@ -26,6 +26,9 @@ __all__ = [
     "gelu_fwd",
     "hip_ops",
     "layernorm_bwd",
+    "linear_dx",
+    "linear_dx_gelu_bwd",
+    "linear_fwd",
     "sumsq",
 ]
 
@@ -131,6 +134,35 @@ def attn_bwd(dout, qkv, out, lse, bsz: int, seqlen: int, n_heads: int, dropout=(
     if qkv_bias_grad is not None:
         ref.colsum_accum(dqkv, qkv_bias_grad)
     return dqkv
+
+
+def _fgemm_ok(k: int, n: int) -> bool:
+    """Shapes the fused MFMA GEMM (csrc/gemm_fused.hip) takes: K % 64 == 0, K >= 256, N % 8 == 0."""
+    return k % 64 == 0 and k >= 256 and n % 8 == 0
+
+
+def linear_fwd(x, w, bias=None):
+    """``x @ w^T + bias`` (nn.Linear forward, bf16 out).  GPU: the fused MFMA GEMM with the bias in
+    its epilogue where the shape allows, else hipBLASLt."""
+    if _on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x.shape[1], w.shape[0]):
+        return hip_ops().gemm_fused(x, w, False, 0, bias)[0]
+    return torch.mm(x, w.t()) if bias is None else torch.addmm(bias, x, w.t())
+
+
+def linear_dx(dy, w):
+    """``dy @ w`` (data gradient of nn.Linear with weight ``w [out, in]``)."""
+    if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy.shape[1], w.shape[1]):
+        return hip_ops().gemm_fused(dy, w, True, 0)[0]
+    return torch.mm(dy, w)
+
+
+def linear_dx_gelu_bwd(dy, w, u, dbias=None):
+    """``du = (dy @ w) * gelu'(u)`` and ``dbias += colsum(du)``: the data gradient of the MLP
+    projection fused with the GELU backward and the fc bias gradient (one GEMM epilogue on GPU
+    instead of a GEMM plus a full read-modify pass over the [M, d_ff] activations)."""
+    if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy.shape[1], w.shape[1]):
+        return hip_ops().gemm_fused(dy, w, True, 2, None, u, dbias)[0]
+    return gelu_bwd(torch.mm(dy, w), u, dbias)
 
 
 def wgrad_accum(dst, dy, x) -> None:

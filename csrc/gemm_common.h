@@ -12,6 +12,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short short4v __attribute__((ext_vector_type(4)));
 typedef short short8v __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) short4v lds_short4;
 typedef __attribute__((address_space(3))) void lds_void;
 

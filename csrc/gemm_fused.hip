@@ -155,6 +155,20 @@ __device__ __forceinline__ void wait_ring(bool post) {
 
 __device__ __forceinline__ bf16x8 lds_b128(const bf16_raw* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
+// 16x16x32 operand from a [k rows][W cols] image with k running down the rows: lane l -> column
+// col0 + (l & 15), elements j = 0..7 -> rows row0 + 8*(l >> 4) + j (two ds_read_b64_tr_b16: in
+// each 16-lane group lane 4q+p addresses row r+q, columns 4p..4p+3)
+template <int W>
+__device__ __forceinline__ bf16x8 tr_frag16(const bf16_raw* tile, int row0, int col0, int lane) {
+  const int i = lane & 15;
+  const int row = row0 + 8 * (lane >> 4) + (i >> 2);
+  const int col = col0 + 4 * (i & 3);
+  const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(tile + swz_off<W>(row, col)));
+  const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(tile + swz_off<W>(row + 4, col)));
+  const short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 // element offset of (row, 16-byte chunk c) in a [rows][64] image (128-byte rows) with the chunk
 // XOR-swizzled by G(row) = g((row >> 1) & 7), g(k) = ((k & 1) << 2) | (k >> 1): the 16 rows of a
 // ds_read_b128 lane group are distinct mod 16, and G spreads them over all 16 bank slots
@@ -282,24 +296,30 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
   // stage g computes).  Iteration g runs its four k16 MFMA groups with every fragment read issued
   // one group ahead; before the last group: wait stage g+1 + retire reads + barrier, DMA stage g+2
   // into the slot stage g vacated, read the first fragments of stage g+1.
-  auto read_frags = [&](int g, int ks, bf16x8 (&af)[4], bf16x8 (&bfr)[2]) {
+  // 16x16x32 MFMAs (at equal cycles per FLOP they hold a higher clock than 32x32x16 on random
+  // data).  A stage (64 k) = 2 k32 steps x 2 halves of the wave's 8 m-fragments = 4 sub-groups of
+  // 16 MFMAs; A fragments double-buffered per sub-group, B fragments per k32 step.
+  auto read_a = [&](int g, int s2, int mh, bf16x8 (&af)[4]) {
     const bf16_raw* aimg = smem + (g % NSLOT) * kSlotElems;
-    const bf16_raw* bimg = aimg + kAElems;
-    const int c = 2 * ks + (lane >> 5);
+    const int c = 4 * s2 + (lane >> 4);
 #pragma unroll
-    for (int b = 0; b < 4; ++b) af[b] = lds_b128(aimg + k64_off(wm * 128 + 32 * b + (lane & 31), c));
+    for (int i = 0; i < 4; ++i) af[i] = lds_b128(aimg + k64_off(wm * 128 + 64 * mh + 16 * i + (lane & 15), c));
+  };
+  auto read_b = [&](int g, int s2, bf16x8 (&bfr)[4]) {
+    const bf16_raw* bimg = smem + (g % NSLOT) * kSlotElems + kAElems;
+    const int c = 4 * s2 + (lane >> 4);
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      if (NN) bfr[a] = tr_frag<BN>(bimg, 16 * ks, wn * 64 + 32 * a, lane);
-      else bfr[a] = lds_b128(bimg + k64_off(wn * 64 + 32 * a + (lane & 31), c));
+    for (int j = 0; j < 4; ++j) {
+      if (NN) bfr[j] = tr_frag16<BN>(bimg, 32 * s2, wn * 64 + 16 * j, lane);
+      else bfr[j] = lds_b128(bimg + k64_off(wn * 64 + 16 * j + (lane & 15), c));
     }
   };
-  auto mfma_group = [&](f32x16 (&acc)[2][4], const bf16x8 (&af)[4], const bf16x8 (&bfr)[2]) {
+  auto mfma_group = [&](f32x4 (&acc)[4][8], int mh, const bf16x8 (&af)[4], const bf16x8 (&bfr)[4]) {
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int b = 0; b < 4; ++b)
-        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[a], af[b], acc[a][b], 0, 0, 0);
+      for (int i = 0; i < 4; ++i)
+        acc[j][4 * mh + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[j][4 * mh + i], 0, 0, 0);
   };
 
   issue(0);
@@ -309,31 +329,34 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
   } else {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
-  bf16x8 af0[4], bf0[2], af1[4], bf1[2];
-  read_frags(0, 0, af0, bf0);
+  bf16x8 a0[4], a1[4], b0[4], b1[4];
+  read_a(0, 0, 0, a0);
+  read_b(0, 0, b0);
 
   int g = 0;  // global stage index of the stream
   for (int t = 0; t < my_tiles; ++t) {
-    f32x16 acc[2][4];  // [n-tile a][m-tile b]
+    f32x4 acc[4][8];  // [n-fragment j][m-fragment i], 16x16 each
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] = 0.f;
+      for (int i = 0; i < 8; ++i) acc[j][i] = 0.f;
 
     for (int s = 0; s < nst; ++s, ++g) {
-      read_frags(g, 1, af1, bf1);
-      mfma_group(acc, af0, bf0);
-      read_frags(g, 2, af0, bf0);
-      mfma_group(acc, af1, bf1);
-      read_frags(g, 3, af1, bf1);
-      mfma_group(acc, af0, bf0);
+      read_a(g, 0, 1, a1);
+      mfma_group(acc, 0, a0, b0);
+      read_a(g, 1, 0, a0);
+      read_b(g, 1, b1);
+      mfma_group(acc, 1, a1, b0);
+      read_a(g, 1, 1, a1);
+      mfma_group(acc, 0, a0, b1);
       if (g + 1 < total) {
         // stage g+1 was issued last, in iteration g-1; an epilogue after it iff g starts a tile
         wait_ring<EpiOps<EPI>::value>(t > 0 && s == 0);
         if (g + 2 < total) issue(g + 2);
-        read_frags(g + 1, 0, af0, bf0);
+        read_a(g + 1, 0, 0, a0);
+        read_b(g + 1, 0, b0);
       }
-      mfma_group(acc, af1, bf1);
+      mfma_group(acc, 1, a1, b1);
     }
 
     // ---------------- epilogue of tile t ----------------
@@ -365,13 +388,17 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
         __builtin_amdgcn_sched_barrier(0);
-        const int row = lane & 31;
+        // 16x16 tile (m-fragment 2b+mi, n-fragment 2a+nj): lane -> row 16 mi + (lane & 15),
+        // its 4 registers -> columns 16 nj + 4 (lane >> 4) .. +3
 #pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const int ch = 2 * gq + (lane >> 5);
-          const f32x16& v = acc[a][b];
-          *reinterpret_cast<float4_t*>(epi + row * 32 + 4 * (ch ^ (row & 7))) =
-              float4_t{v[4 * gq], v[4 * gq + 1], v[4 * gq + 2], v[4 * gq + 3]};
+        for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+          for (int nj = 0; nj < 2; ++nj) {
+            const int row = 16 * mi + (lane & 15);
+            const int ch = 4 * nj + (lane >> 4);
+            const f32x4& v = acc[2 * a + nj][2 * b + mi];
+            *reinterpret_cast<float4_t*>(epi + row * 32 + 4 * (ch ^ (row & 7))) = float4_t{v[0], v[1], v[2], v[3]};
+          }
         }
         __builtin_amdgcn_sched_barrier(0);  // wave-local: LDS executes a wave's ops in order
         float4_t vals[4];

@@ -11,6 +11,16 @@
 
 #include "kernels.h"  // DropoutArgs
 
+// Device-side bounds checks of the debug build (`python -m llmtrain.ops.build --debug`,
+// -DLLMT_DEBUG=1): a failing check aborts the kernel with file/line instead of silently reading
+// or writing out of bounds.  Compiled out of the release build.
+#if defined(LLMT_DEBUG) && LLMT_DEBUG
+#include <cassert>
+#define LLMT_DASSERT(cond) assert(cond)
+#else
+#define LLMT_DASSERT(cond) ((void)0)
+#endif
+
 namespace llmt {
 
 constexpr int kWave = 64;

@@ -58,6 +58,7 @@ __global__ __launch_bounds__(kCeThreads) void ce_fwd_bwd_kernel(
   T* z = logits + row * (long)Vp;
   const int nvec = Vp >> 3;
   const int64_t label = labels[row];
+  LLMT_DASSERT(label < V);  // negative = ignored row; >= V is a data bug
   const bool valid = label >= 0 && label < V;
   const float t_label = valid ? scalar_f(z[label]) * kLog2e : 0.f;  // read before any write
 

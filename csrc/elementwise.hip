@@ -143,7 +143,8 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __res
   if (row >= M) return;
   const int lane = threadIdx.x & 63;
   long tok = ids[row];
-  tok = tok < 0 ? 0 : (tok >= V ? V - 1 : tok);  // clamp: never read out of bounds
+  LLMT_DASSERT(tok >= 0 && tok < V);              // debug build: report bad token ids
+  tok = tok < 0 ? 0 : (tok >= V ? V - 1 : tok);  // release: clamp, never read out of bounds
   const int t = (int)(row % T);
   const float4_t* e = reinterpret_cast<const float4_t*>(wte + tok * (long)d);
   const float4_t* p = reinterpret_cast<const float4_t*>(wpe + (long)t * d);
@@ -169,6 +170,7 @@ __global__ __launch_bounds__(256) void embedding_bwd_tok_kernel(const float* __r
   if (row >= M) return;
   const int lane = threadIdx.x & 63;
   const long tok = ids[row];
+  LLMT_DASSERT(tok >= 0 && tok < V);
   if (tok < 0 || tok >= V) return;
   const float* src = dx + row * (long)d;
   float* dst = dwte + tok * (long)d;

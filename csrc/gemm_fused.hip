@@ -263,6 +263,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
       mt = r / wl;
       nt = full * kBand + (r - mt * wl);
     }
+    LLMT_DASSERT(mt < p.tiles_m && nt < p.tiles_n);
     m0 = mt * BM;
     n0 = nt * BN;
   };

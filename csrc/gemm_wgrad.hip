@@ -77,6 +77,7 @@ __global__ __launch_bounds__(kThreads, (Cfg<TN, TK>::kMinBlocks)) void wgrad_ker
   const int chunk = w / tiles, tile = w - chunk * tiles;
   const int tile_n = tile / tiles_k, tile_k = tile - tile_n * tiles_k;
   const int n0 = tile_n * G::BN, k0 = tile_k * G::BK;
+  LLMT_DASSERT(n0 < N && k0 < K);
   const int m_begin = chunk * m_chunk;
   const int rows = min(M - m_begin, m_chunk);
   if (rows <= 0) return;

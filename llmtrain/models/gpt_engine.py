@@ -191,6 +191,7 @@ class FusedGPTEngine:
         # dX with the GELU backward + fc-bias gradient in its epilogue, and the attention output
         # projection forward/dX (LLMTRAIN_FUSED_GEMM=0: hipBLASLt + separate GELU backward)
         self.fused_gemm = os.environ.get("LLMTRAIN_FUSED_GEMM", "1") != "0"
+        self.markers = os.environ.get("LLMTRAIN_ROCTX", "0") == "1" and self.store.device.type == "cuda"
         self._side: torch.cuda.Stream | None = None
         self._pending: list[torch.Tensor] = []  # operands of side-stream GEMMs of the current block
         self._held: list[tuple[Any, list[torch.Tensor]]] = []  # (side event, operands) per block
@@ -283,6 +284,17 @@ class FusedGPTEngine:
         loss, _ = self._forward(ids, labels, mask, keep=False)
         return loss
 
+    def _push(self, name: str) -> None:
+        """Open a roctx range (``torch.cuda.nvtx`` is roctx on ROCm) around an engine phase when
+        ``LLMTRAIN_ROCTX=1``: ``rocprofv3 --marker-trace`` / torch.profiler then show the fused
+        step per block instead of a flat kernel list."""
+        if self.markers:
+            torch.cuda.nvtx.range_push(name)
+
+    def _pop(self) -> None:
+        if self.markers:
+            torch.cuda.nvtx.range_pop()
+
     # -- forward ---------------------------------------------------------------------------
 
     def _forward(self, ids, labels, mask, *, keep: bool):
@@ -305,9 +317,12 @@ class FusedGPTEngine:
         else:
             row_w = torch.full((n_tok,), 1.0 / n_tok, dtype=torch.float32, device=ids.device)
 
+        self._push("fwd.embed")
         x = ops.embedding_fwd(ids, m.token_embedding.weight, m.position_embedding.weight, dropout=state.site(0))
+        self._pop()
         delta: torch.Tensor | None = None
         for i, blk in enumerate(self.blocks):
+            self._push(f"fwd.block{i}")
             xs, h1, mu1, rs1 = ops.add_layernorm_fwd(
                 x, delta, blk.ln_1.weight, blk.ln_1.bias, self.eps, cdt, dropout=state.site(3 * i)
             )  # site 3i = the previous block's MLP branch (unused for block 0: delta is None)
@@ -323,7 +338,9 @@ class FusedGPTEngine:
             x = xm
             if keep:
                 state.blocks.append(_BlockActs(xs, h1, mu1, rs1, qkv, att, lse, xm, h2, mu2, rs2, u, g))
+            self._pop()
         n_layers = len(self.blocks)
+        self._push("fwd.head_ce")
         xf, hf, muf, rsf = ops.add_layernorm_fwd(
             x, delta, m.ln_f.weight, m.ln_f.bias, self.eps, cdt, dropout=state.site(3 * n_layers)
         )
@@ -331,6 +348,7 @@ class FusedGPTEngine:
         logits = torch.mm(hf, head.t())  # [M, Vp]
         per_row = ops.cross_entropy_fwd_bwd(logits, labels.reshape(-1), self.vocab, row_w)
         loss = torch.dot(per_row, row_w)
+        self._pop()
         if keep:
             state.xf, state.hf, state.muf, state.rsf = xf, hf, muf, rsf
             state.dlogits = logits
@@ -359,12 +377,12 @@ class FusedGPTEngine:
         dlogits = st.dlogits
         assert dlogits is not None and st.hf is not None
         head = self.store.shadow_of(self.head_weight, padded=True)
+        self._push("bwd.head")
 
-        # LM head: dhf = dlogits @ W ; dW += dlogits^T @ (go * hf).  The weight gradient runs on
-        # the side stream, overlapping the last blocks' bandwidth-bound backward kernels.  No
-        # record_stream (it would pin the multi-GB dlogits block past the step and force fresh
-        # allocations every step): the engine holds dlogits until the main stream has joined the
-        # side stream at the end of the backward, so its memory is reused only after the GEMM.
+        # LM head: dhf = dlogits @ W ; dW += dlogits^T @ (go * hf).  With LLMTRAIN_HEAD_WGRAD_SIDE=1
+        # the weight gradient runs on the side stream; no record_stream then (it would pin the
+        # multi-GB dlogits block past the step and force fresh allocations every step): the engine
+        # holds dlogits until the main stream has joined the side stream at the end of the backward.
         dhf = torch.mm(dlogits, head)
         hf_scaled = (st.hf.float() * go).to(st.hf.dtype) if st.hf.dtype != torch.float32 else st.hf * go
         side = self._side_stream() if self.head_wgrad_side else None
@@ -389,7 +407,9 @@ class FusedGPTEngine:
         del dhf
         self._notify("ln_f")
 
+        self._pop()
         for i in reversed(range(len(self.blocks))):
+            self._push(f"bwd.block{i}")
             blk, a = self.blocks[i], st.blocks[i]
             # MLP: delta = g Wp^T + bp ; dx is d(delta) (bias grad already summed by the LN bwd)
             self._wgrad(self._g(blk.mlp_proj.weight), dx_lp, a.g)
@@ -430,6 +450,7 @@ class FusedGPTEngine:
             st.blocks[i] = None  # type: ignore[call-overload]  # free activations early
             self._notify(f"block{i}")
             self._retire_block()
+            self._pop()
 
         ops.embedding_bwd(
             dx, st.ids, self._g(m.token_embedding.weight), self._g(m.position_embedding.weight), dropout=st.site(0)

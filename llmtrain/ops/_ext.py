@@ -19,6 +19,7 @@ import torch
 __all__ = ["EXT_PATH", "is_loaded", "load", "require"]
 
 EXT_PATH = Path(__file__).with_name("_llmtrain_hip.so")
+DEBUG_EXT_PATH = Path(__file__).with_name("_llmtrain_hip_debug.so")
 _lock = threading.Lock()
 _state: dict[str, object] = {"loaded": False, "error": None}
 
@@ -30,7 +31,8 @@ def load() -> bool:
             return True
         if _state["error"] is not None:
             return False
-        path = Path(os.environ.get("LLMTRAIN_HIP_EXT", EXT_PATH))
+        default = DEBUG_EXT_PATH if os.environ.get("LLMTRAIN_DEBUG_KERNELS", "0") == "1" else EXT_PATH
+        path = Path(os.environ.get("LLMTRAIN_HIP_EXT", default))
         if not path.exists():
             _state["error"] = f"{path} not found (build it with `python -m llmtrain.ops.build`)"
             return False

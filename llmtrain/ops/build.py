@@ -23,11 +23,14 @@ from pathlib import Path
 
 import torch
 
-__all__ = ["build", "CSRC", "OUT"]
+__all__ = ["build", "CSRC", "OUT", "OUT_DEBUG"]
 
 REPO = Path(__file__).resolve().parents[2]
 CSRC = REPO / "csrc"
 OUT = Path(__file__).resolve().with_name("_llmtrain_hip.so")
+# `--debug`: -O1 -g with device-side bounds asserts (LLMT_DASSERT in csrc/common.h); loaded instead
+# of the release object when LLMTRAIN_DEBUG_KERNELS=1 (see llmtrain/ops/_ext.py)
+OUT_DEBUG = Path(__file__).resolve().with_name("_llmtrain_hip_debug.so")
 OBJDIR = REPO / "build" / "hip_obj"
 ARCH = os.environ.get("LLMTRAIN_OFFLOAD_ARCH", "gfx950")
 
@@ -102,21 +105,22 @@ def build(*, jobs: int | None = None, force: bool = False, debug: bool = False, 
     with ThreadPoolExecutor(max_workers=jobs) as pool:
         objs = list(pool.map(lambda s: _compile(s, debug, force), sources))
     newest = max(o.stat().st_mtime for o in objs)
-    if force or not OUT.exists() or OUT.stat().st_mtime < newest:
+    out = OUT_DEBUG if debug else OUT
+    if force or not out.exists() or out.stat().st_mtime < newest:
         _, lib = _torch_dirs()
         cmd = [
             _hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), f"-L{lib}",
             "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-lc10", "-lc10_hip",
-            f"-Wl,-rpath,{lib}", "-o", str(OUT),
+            f"-Wl,-rpath,{lib}", "-o", str(out),
         ]
         proc = subprocess.run(cmd, capture_output=True, text=True)
         if proc.returncode != 0:
             raise RuntimeError(f"link failed:\n{proc.stdout}\n{proc.stderr}")
         if verbose:
-            print(f"[llmtrain.ops.build] linked {OUT} ({OUT.stat().st_size / 2**20:.1f} MiB, {ARCH})")
+            print(f"[llmtrain.ops.build] linked {out} ({out.stat().st_size / 2**20:.1f} MiB, {ARCH})")
     elif verbose:
-        print(f"[llmtrain.ops.build] {OUT} up to date")
-    return OUT
+        print(f"[llmtrain.ops.build] {out} up to date")
+    return out
 
 
 def main(argv: list[str] | None = None) -> int:

@@ -170,12 +170,10 @@ __device__ __forceinline__ bf16x8 tr_frag16(const bf16_raw* tile, int row0, int 
 }
 
 // element offset of (row, 16-byte chunk c) in a [rows][64] image (128-byte rows) with the chunk
-// XOR-swizzled by G(row) = g((row >> 1) & 7), g(k) = ((k & 1) << 2) | (k >> 1): the 16 rows of a
-// ds_read_b128 lane group are distinct mod 16, and G spreads them over all 16 bank slots
-__device__ __forceinline__ int swz_g(int row) {
-  const int k = (row >> 1) & 7;
-  return ((k & 1) << 2) | (k >> 1);
-}
+// XOR-swizzled by G(row) = row & 7.  A 16x16x32 fragment read (ds_read_b128) puts rows r0..r0+15
+// on lanes 0-15 (chunk c) and again on lanes 16-31 (chunk c+1); each hardware lane group of 16
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) then covers all 16 bank slots exactly once.
+__device__ __forceinline__ int swz_g(int row) { return row & 7; }
 __device__ __forceinline__ int k64_off(int row, int c) { return row * 64 + 8 * (c ^ swz_g(row)); }
 
 struct Args {

@@ -357,6 +357,9 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tens
   TORCH_CHECK((b_kn ? b.size(0) : b.size(1)) == K, "gemm_fused: inner dimensions differ");
   TORCH_CHECK(K % 64 == 0 && K >= 256 && N % 8 == 0, "gemm_fused: needs K % 64 == 0, K >= 256, N % 8 == 0");
   TORCH_CHECK(epilogue >= 0 && epilogue <= 2, "gemm_fused: epilogue must be 0, 1 or 2");
+  // 16-byte LDS-DMA / vector stores on every operand, 4-byte DMA of the bias
+  TORCH_CHECK((uintptr_t)a.data_ptr() % 16 == 0 && (uintptr_t)b.data_ptr() % 16 == 0,
+              "gemm_fused: operands must be 16-byte aligned");
   at::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
   llmt::GemmFusedArgs g;
   g.a = a.data_ptr();
@@ -376,6 +379,7 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tens
     check_gpu(*bias, "bias");
     check_dtype(*bias, at::kBFloat16, "bias");
     TORCH_CHECK(bias->numel() == N, "gemm_fused: bias must have N elements");
+    TORCH_CHECK((uintptr_t)bias->data_ptr() % 4 == 0, "gemm_fused: bias must be 4-byte aligned");
     g.bias = bias->data_ptr();
   }
   if (epilogue == 1) {
@@ -387,6 +391,7 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tens
     check_gpu(*u, "u");
     check_dtype(*u, at::kBFloat16, "u");
     TORCH_CHECK(u->dim() == 2 && u->size(0) == M && u->size(1) == N, "gemm_fused: u must be [M, N]");
+    TORCH_CHECK((uintptr_t)u->data_ptr() % 16 == 0, "gemm_fused: u must be 16-byte aligned");
     g.u = u->data_ptr();
     g.ldu = (int)N;
     if (dbias.has_value()) {

@@ -53,7 +53,7 @@ constexpr int kSlotElems = kAElems + kBElems;   // 64 KiB
 constexpr int kDmaA = kAElems * 2 / 1024 / kWaves;  // 1-KiB DMA ops per wave per stage (4)
 constexpr int kDmaB = kBElems * 2 / 1024 / kWaves;  // (4)
 constexpr int P = kDmaA + kDmaB;                // 8
-constexpr int kEpiFloats = 32 * 32;             // per-wave fp32 staging image [32][32] (4 KiB)
+constexpr int kEpiFloats = 16 * 64;             // per-wave fp32 staging image [16][64] (4 KiB)
 constexpr int kSmemElems = NSLOT * kSlotElems + kWaves * kEpiFloats * 2;  // 160 KiB
 constexpr int kOob = 0x7ffffff0;                // buffer offset past any descriptor: dropped / 0
 constexpr int kBand = 4;                        // n-tiles per raster band (see tile_origin)
@@ -85,7 +85,7 @@ __device__ __forceinline__ float gelu_grad(float u) {
 // VMEM ops each epilogue issues unconditionally (a lower bound is what the counted waits need)
 template <int EPI>
 struct EpiOps {
-  static constexpr int value = EPI == 0 ? 32 : 64;
+  static constexpr int value = EPI == 0 ? 16 : 32;
 };
 
 // one 256-byte LDS-DMA op (4 bytes per lane), M0 saved/restored like dma16
@@ -187,6 +187,7 @@ struct Args {
   int lda, ldb, ldc, ldu;
   int M, N, K;
   int tiles_m, tiles_n, ntiles, nwg;
+  int band;  // n-tiles per raster band (tile_origin)
   int debug;
 };
 
@@ -250,16 +251,17 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
   // whole weight from the Infinity Cache every round).
   auto tile_origin = [&](int t, int& m0, int& n0) {
     const int w = base + jx + t * wgx;
-    const int full = p.tiles_n / kBand, per_band = p.tiles_m * kBand;
+    const int band = p.band;
+    const int full = p.tiles_n / band, per_band = p.tiles_m * band;
     int mt, nt;
     if (w < full * per_band) {
       const int b = w / per_band, r = w - b * per_band;
-      mt = r / kBand;
-      nt = b * kBand + (r - mt * kBand);
+      mt = r / band;
+      nt = b * band + (r - mt * band);
     } else {
-      const int wl = p.tiles_n - full * kBand, r = w - full * per_band;
+      const int wl = p.tiles_n - full * band, r = w - full * per_band;
       mt = r / wl;
-      nt = full * kBand + (r - mt * wl);
+      nt = full * band + (r - mt * wl);
     }
     LLMT_DASSERT(mt < p.tiles_m && nt < p.tiles_n);
     m0 = mt * BM;
@@ -359,118 +361,104 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
     }
 
     // ---------------- epilogue of tile t ----------------
-    // per 32x32 accumulator tile: registers -> [32 m][32 n] fp32 LDS image (16-byte chunks XOR
-    // (row & 7)) -> 8 rows x 4 columns per lane-octet read back -> 8-byte row segments
+    // per 16-row m-fragment: its four 16x16 accumulator tiles -> [16 m][64 n] fp32 LDS image
+    // (16-byte chunks XOR (row & 15)) -> 8 lanes per row read 8 columns each -> one 16-byte store
+    // per lane, a wave instruction writing 8 whole 128-byte row segments
     int m0, n0;
     tile_origin(t, m0, n0);
     const int mw = m0 + wm * 128, nw = n0 + wn * 64;
-    const int q = lane & 7;  // this lane's 4-column group within a 32-column tile
-    float bias_f[2][4];
-    float csum[2][4];
+    const int q = lane & 7;  // this lane's 8-column group of the wave's 64 columns
+    const int n = nw + 8 * q;
+    float bias_f[8];
+    float csum[8];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        bias_f[a][k] = 0.f;
-        csum[a][k] = 0.f;
-      }
+    for (int k = 0; k < 8; ++k) {
+      bias_f[k] = 0.f;
+      csum[k] = 0.f;
+    }
     if (kBiasDma) {
+      const ushort8_t bv = *reinterpret_cast<const ushort8_t*>(reinterpret_cast<const bf16_raw*>(epi) + 8 * q);
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        const ushort4_t bv = *reinterpret_cast<const ushort4_t*>(reinterpret_cast<const bf16_raw*>(epi) + 32 * a + 4 * q);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) bias_f[a][k] = bf2f(bv[k]);
-      }
+      for (int k = 0; k < 8; ++k) bias_f[k] = bf2f(bv[k]);
     }
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
+    for (int mf = 0; mf < 8; ++mf) {
+      __builtin_amdgcn_sched_barrier(0);
+      {
+        const int row = lane & 15;
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        __builtin_amdgcn_sched_barrier(0);
-        // 16x16 tile (m-fragment 2b+mi, n-fragment 2a+nj): lane -> row 16 mi + (lane & 15),
-        // its 4 registers -> columns 16 nj + 4 (lane >> 4) .. +3
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi) {
-#pragma unroll
-          for (int nj = 0; nj < 2; ++nj) {
-            const int row = 16 * mi + (lane & 15);
-            const int ch = 4 * nj + (lane >> 4);
-            const f32x4& v = acc[2 * a + nj][2 * b + mi];
-            *reinterpret_cast<float4_t*>(epi + row * 32 + 4 * (ch ^ (row & 7))) = float4_t{v[0], v[1], v[2], v[3]};
-          }
+        for (int nf = 0; nf < 4; ++nf) {
+          const int ch = 4 * nf + (lane >> 4);
+          const f32x4& v = acc[nf][mf];
+          *reinterpret_cast<float4_t*>(epi + row * 64 + 4 * (ch ^ row)) = float4_t{v[0], v[1], v[2], v[3]};
         }
-        __builtin_amdgcn_sched_barrier(0);  // wave-local: LDS executes a wave's ops in order
-        float4_t vals[4];
-        int off[4];
+      }
+      __builtin_amdgcn_sched_barrier(0);  // wave-local: LDS executes a wave's ops in order
+      float vals[2][8];
+      int off[2];
 #pragma unroll
-        for (int it = 0; it < 4; ++it) {
-          const int R = 8 * it + (lane >> 3);
-          vals[it] = *reinterpret_cast<const float4_t*>(epi + R * 32 + 4 * (q ^ (R & 7)));
-          const int m = mw + 32 * b + R, n = nw + 32 * a + 4 * q;
-          off[it] = (m < p.M && n < p.N) ? (m * p.ldc + n) * 2 : kOob;
+      for (int it = 0; it < 2; ++it) {
+        const int R = 8 * it + (lane >> 3);
+        const float4_t lo = *reinterpret_cast<const float4_t*>(epi + R * 64 + 4 * ((2 * q) ^ R));
+        const float4_t hi = *reinterpret_cast<const float4_t*>(epi + R * 64 + 4 * ((2 * q + 1) ^ R));
+        vals[it][0] = lo[0]; vals[it][1] = lo[1]; vals[it][2] = lo[2]; vals[it][3] = lo[3];
+        vals[it][4] = hi[0]; vals[it][5] = hi[1]; vals[it][6] = hi[2]; vals[it][7] = hi[3];
+        const int m = mw + 16 * mf + R;
+        off[it] = (m < p.M && n < p.N) ? (m * p.ldc + n) * 2 : kOob;
+      }
+      asm volatile("" ::: "memory");
+      if (EPI == 2) {
+        u32x4 uraw[2];
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          const int m = mw + 16 * mf + 8 * it + (lane >> 3);
+          const int uoff = (m < p.M && n < p.N) ? (m * p.ldu + n) * 2 : kOob;
+          uraw[it] = __builtin_amdgcn_raw_buffer_load_b128(ru, uoff, 0, 0);
         }
-        asm volatile("" ::: "memory");
-        if (EPI == 2) {
-          u32x2 uraw[4];
 #pragma unroll
-          for (int it = 0; it < 4; ++it) {
-            const int R = 8 * it + (lane >> 3);
-            const int m = mw + 32 * b + R, n = nw + 32 * a + 4 * q;
-            const int uoff = (m < p.M && n < p.N) ? (m * p.ldu + n) * 2 : kOob;
-            uraw[it] = __builtin_amdgcn_raw_buffer_load_b64(ru, uoff, 0, 0);
+        for (int it = 0; it < 2; ++it) {
+          __builtin_amdgcn_sched_barrier(0);  // one row segment at a time: bounded VGPR pressure
+          const ushort8_t uv = __builtin_bit_cast(ushort8_t, uraw[it]);
+          float o[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            o[k] = bf2f(f2bf(vals[it][k] * gelu_grad(bf2f(uv[k]))));
+            csum[k] += o[k];
           }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(o)), rc, off[it], 0, 0);
+          // pin the running sums here: left alone, hipcc sinks the adds to the end of the epilogue
+          // and keeps every product live (spills)
+          asm volatile("" : "+v"(csum[0]), "+v"(csum[1]), "+v"(csum[2]), "+v"(csum[3]), "+v"(csum[4]),
+                       "+v"(csum[5]), "+v"(csum[6]), "+v"(csum[7]));
+        }
+      } else {
 #pragma unroll
-          for (int it = 0; it < 4; ++it) {
-            __builtin_amdgcn_sched_barrier(0);  // one row segment at a time: bounded VGPR pressure
-            const ushort4_t uv = __builtin_bit_cast(ushort4_t, uraw[it]);
-            ushort4_t ov;
+        for (int it = 0; it < 2; ++it) {
+          float o[8];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              ov[k] = f2bf(vals[it][k] * gelu_grad(bf2f(uv[k])));
-              csum[a][k] += bf2f(ov[k]);
-            }
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, ov), rc, off[it], 0, 0);
-            // pin the running sums here: left alone, hipcc sinks all the adds to the end of the
-            // epilogue and keeps every product live (spills)
-            asm volatile("" : "+v"(csum[a][0]), "+v"(csum[a][1]), "+v"(csum[a][2]), "+v"(csum[a][3]));
-          }
-        } else {
+          for (int k = 0; k < 8; ++k) o[k] = vals[it][k] + bias_f[k];
+          const ushort8_t ov = pack8(o);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ov), rc, off[it], 0, 0);
+          if (EPI == 1) {
 #pragma unroll
-          for (int it = 0; it < 4; ++it) {
-            ushort4_t ov;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) ov[k] = f2bf(vals[it][k] + bias_f[a][k]);
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, ov), rc, off[it], 0, 0);
-            if (EPI == 1) {
-              ushort4_t gv;
-#pragma unroll
-              for (int k = 0; k < 4; ++k) gv[k] = f2bf(gelu(bf2f(ov[k])));
-              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, gv), rc2, off[it], 0, 0);
-            }
+            for (int k = 0; k < 8; ++k) o[k] = gelu(bf2f(ov[k]));
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(o)), rc2, off[it], 0, 0);
           }
         }
       }
     }
-    if (EPI == 2 && p.dbias != nullptr) {
+    if (EPI == 2 && p.dbias != nullptr) {  // column sums over the wave's 128 rows: lanes sharing q
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+      for (int k = 0; k < 8; ++k) {
+        float v = csum[k];
+        v += __shfl_xor(v, 8, 64);
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        csum[k] = v;
+      }
+      if (lane < 8 && n < p.N) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          float v = csum[a][k];
-          v += __shfl_xor(v, 8, 64);
-          v += __shfl_xor(v, 16, 64);
-          v += __shfl_xor(v, 32, 64);
-          csum[a][k] = v;
-        }
-      if (lane < 8) {
-#pragma unroll
-        for (int a = 0; a < 2; ++a) {
-          const int n = nw + 32 * a + 4 * q;
-          if (n < p.N) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) atomicAdd(p.dbias + n + k, csum[a][k]);
-          }
-        }
+        for (int k = 0; k < 8; ++k) atomicAdd(p.dbias + n + k, csum[k]);
       }
     }
   }
@@ -520,6 +508,11 @@ hipError_t launch_gemm_fused(const GemmFusedArgs& g, hipStream_t stream) {
     return e ? std::atoi(e) : 0;
   }();
   a.debug = debug;
+  static const int band_env = [] {
+    const char* e = std::getenv("LLMT_FGEMM_BAND");
+    return e ? std::atoi(e) : 0;
+  }();
+  a.band = band_env > 0 ? (band_env < a.tiles_n ? band_env : a.tiles_n) : (kBand < a.tiles_n ? kBand : a.tiles_n);
   switch (g.epilogue * 2 + (g.b_kn ? 1 : 0)) {
     case 0: launch_one<false, 0>(a, stream); break;
     case 1: launch_one<true, 0>(a, stream); break;

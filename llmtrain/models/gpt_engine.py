@@ -187,10 +187,13 @@ class FusedGPTEngine:
         # weight-gradient GEMMs on a second HIP stream, overlapping the dX GEMMs and the
         # bandwidth-bound backward kernels of the main stream (LLMTRAIN_WGRAD_STREAM=0 disables)
         self.wgrad_stream_enabled = os.environ.get("LLMTRAIN_WGRAD_STREAM", "1") != "0"
-        # hand-written MFMA GEMM (csrc/gemm_fused.hip) where it beats hipBLASLt: the MLP projection's
-        # dX with the GELU backward + fc-bias gradient in its epilogue, and the attention output
-        # projection forward/dX (LLMTRAIN_FUSED_GEMM=0: hipBLASLt + separate GELU backward)
-        self.fused_gemm = os.environ.get("LLMTRAIN_FUSED_GEMM", "1") != "0"
+        # hand-written MFMA GEMM (csrc/gemm_fused.hip) where it beats hipBLASLt: qkv and attention
+        # output projections (forward and dX), the fc forward with bias + GELU in its epilogue, the
+        # MLP projection dX with the GELU backward + fc-bias gradient in its epilogue
+        # (LLMTRAIN_FUSED_GEMM=0: hipBLASLt everywhere + separate GELU passes)
+        mode = os.environ.get("LLMTRAIN_FUSED_GEMM", "1")
+        self.fused_gemm = mode != "0"  # forward GEMMs
+        self.fused_gemm_bwd = mode not in ("0", "fwd")  # dX GEMMs
         self.markers = os.environ.get("LLMTRAIN_ROCTX", "0") == "1" and self.store.device.type == "cuda"
         self._side: torch.cuda.Stream | None = None
         self._pending: list[torch.Tensor] = []  # operands of side-stream GEMMs of the current block
@@ -326,14 +329,17 @@ class FusedGPTEngine:
             xs, h1, mu1, rs1 = ops.add_layernorm_fwd(
                 x, delta, blk.ln_1.weight, blk.ln_1.bias, self.eps, cdt, dropout=state.site(3 * i)
             )  # site 3i = the previous block's MLP branch (unused for block 0: delta is None)
-            qkv = self._linear(h1, blk.attn.qkv_proj)
+            qkv = self._linear(h1, blk.attn.qkv_proj, fused=True)
             att, lse = ops.attn_fwd(qkv, bsz, seqlen, self.n_heads, dropout=state.site(2 + 3 * i))
             y = self._linear(att, blk.attn.out_proj, fused=True)
             xm, h2, mu2, rs2 = ops.add_layernorm_fwd(
                 xs, y, blk.ln_2.weight, blk.ln_2.bias, self.eps, cdt, dropout=state.site(1 + 3 * i)
             )
-            u = self._linear(h2, blk.mlp_fc)
-            g = ops.gelu_fwd(u)
+            if self.fused_gemm:  # bias + exact-erf GELU in the fc GEMM's epilogue
+                u, g = ops.linear_fwd_gelu(h2, self._w(blk.mlp_fc.weight), self._w(blk.mlp_fc.bias))
+            else:
+                u = self._linear(h2, blk.mlp_fc)
+                g = ops.gelu_fwd(u)
             delta = self._linear(g, blk.mlp_proj)
             x = xm
             if keep:
@@ -413,7 +419,7 @@ class FusedGPTEngine:
             blk, a = self.blocks[i], st.blocks[i]
             # MLP: delta = g Wp^T + bp ; dx is d(delta) (bias grad already summed by the LN bwd)
             self._wgrad(self._g(blk.mlp_proj.weight), dx_lp, a.g)
-            if self.fused_gemm:  # GELU backward + fc bias grad in the dX GEMM's epilogue
+            if self.fused_gemm_bwd:  # GELU backward + fc bias grad in the dX GEMM's epilogue
                 du = ops.linear_dx_gelu_bwd(dx_lp, self._w(blk.mlp_proj.weight), a.u, self._g(blk.mlp_fc.bias))
             else:
                 dg = torch.mm(dx_lp, self._w(blk.mlp_proj.weight))
@@ -430,7 +436,7 @@ class FusedGPTEngine:
             # attention output projection
             self._wgrad(self._g(blk.attn.out_proj.weight), dy_lp, a.att)
             wo = self._w(blk.attn.out_proj.weight)
-            datt = ops.linear_dx(dy_lp, wo) if self.fused_gemm else torch.mm(dy_lp, wo)
+            datt = ops.linear_dx(dy_lp, wo) if self.fused_gemm_bwd else torch.mm(dy_lp, wo)
             del dy_lp
             # the qkv-bias gradient (column sums of dqkv) is fused into the attention backward
             dqkv = ops.attn_bwd(
@@ -439,7 +445,8 @@ class FusedGPTEngine:
             )
             del datt
             self._wgrad(self._g(blk.attn.qkv_proj.weight), dqkv, a.h1)
-            dh1 = torch.mm(dqkv, self._w(blk.attn.qkv_proj.weight))
+            wq = self._w(blk.attn.qkv_proj.weight)
+            dh1 = ops.linear_dx(dqkv, wq) if self.fused_gemm_bwd else torch.mm(dqkv, wq)
             del dqkv
             prev_bias = self._g(self.blocks[i - 1].mlp_proj.bias) if i > 0 else None
             dx, dx_lp = ops.layernorm_bwd(

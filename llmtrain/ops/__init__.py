@@ -8,6 +8,8 @@ op and no silent fallback: a GPU tensor with the extension missing raises (``_ex
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from llmtrain.ops import _ext
@@ -29,6 +31,7 @@ __all__ = [
     "linear_dx",
     "linear_dx_gelu_bwd",
     "linear_fwd",
+    "linear_fwd_gelu",
     "sumsq",
 ]
 
@@ -136,22 +139,45 @@ def attn_bwd(dout, qkv, out, lse, bsz: int, seqlen: int, n_heads: int, dropout=(
     return dqkv
 
 
-def _fgemm_ok(k: int, n: int) -> bool:
-    """Shapes the fused MFMA GEMM (csrc/gemm_fused.hip) takes: K % 64 == 0, K >= 256, N % 8 == 0."""
-    return k % 64 == 0 and k >= 256 and n % 8 == 0
+# Where the fused GEMM pays in a real step (same-box A/B, docs/performance.md): GPT-2 XL micro-batch
+# 16 (A operands 52 MB) +3 %; GPT-2 124M at 64K-128K tokens per step (A 100-600 MB) -1.4 % although
+# each GEMM alone is ahead of hipBLASLt at 64K: its persistent, statically scheduled 160 KiB-LDS
+# workgroups start late on CUs still draining the previous kernel.  Above this many A bytes the
+# engine stays on hipBLASLt.
+FGEMM_MAX_A_BYTES = int(os.environ.get("LLMTRAIN_FGEMM_MAX_A_MB", "64")) * 2**20
+
+
+def _fgemm_ok(a: torch.Tensor, k: int, n: int, *others: torch.Tensor | None) -> bool:
+    """Shapes/placements the fused MFMA GEMM (csrc/gemm_fused.hip) takes and wins on:
+    K % 64 == 0, K >= 256, N % 8 == 0, 16-byte aligned operands, A small enough (see above)."""
+    if not (k % 64 == 0 and k >= 256 and n % 8 == 0):
+        return False
+    if a.numel() * a.element_size() > FGEMM_MAX_A_BYTES:
+        return False
+    return all(t is None or t.data_ptr() % 16 == 0 for t in (a, *others))
 
 
 def linear_fwd(x, w, bias=None):
     """``x @ w^T + bias`` (nn.Linear forward, bf16 out).  GPU: the fused MFMA GEMM with the bias in
     its epilogue where the shape allows, else hipBLASLt."""
-    if _on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x.shape[1], w.shape[0]):
+    if _on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x, x.shape[1], w.shape[0], w, bias):
         return hip_ops().gemm_fused(x, w, False, 0, bias)[0]
     return torch.mm(x, w.t()) if bias is None else torch.addmm(bias, x, w.t())
 
 
+def linear_fwd_gelu(x, w, bias=None):
+    """``u = x @ w^T + bias`` and ``g = gelu(u)`` (exact erf GELU of the bf16 ``u``, which the
+    backward reads): on GPU the GELU rides in the GEMM epilogue, no separate pass over ``u``."""
+    if _on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x, x.shape[1], w.shape[0], w, bias):
+        u, g = hip_ops().gemm_fused(x, w, False, 1, bias)
+        return u, g
+    u = torch.mm(x, w.t()) if bias is None else torch.addmm(bias, x, w.t())
+    return u, gelu_fwd(u)
+
+
 def linear_dx(dy, w):
     """``dy @ w`` (data gradient of nn.Linear with weight ``w [out, in]``)."""
-    if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy.shape[1], w.shape[1]):
+    if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy, dy.shape[1], w.shape[1], w):
         return hip_ops().gemm_fused(dy, w, True, 0)[0]
     return torch.mm(dy, w)
 
@@ -160,7 +186,7 @@ def linear_dx_gelu_bwd(dy, w, u, dbias=None):
     """``du = (dy @ w) * gelu'(u)`` and ``dbias += colsum(du)``: the data gradient of the MLP
     projection fused with the GELU backward and the fc bias gradient (one GEMM epilogue on GPU
     instead of a GEMM plus a full read-modify pass over the [M, d_ff] activations)."""
-    if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy.shape[1], w.shape[1]):
+    if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy, dy.shape[1], w.shape[1], w, u):
         return hip_ops().gemm_fused(dy, w, True, 2, None, u, dbias)[0]
     return gelu_bwd(torch.mm(dy, w), u, dbias)
 

@@ -502,7 +502,14 @@ hipError_t launch_gemm_fused(const GemmFusedArgs& g, hipStream_t stream) {
   a.tiles_m = (g.M + BM - 1) / BM;
   a.ntiles = a.tiles_m * a.tiles_n;
   const int ncu = gemm::cu_count();
-  a.nwg = a.ntiles < ncu ? a.ntiles : ncu;
+  // LLMT_FGEMM_WAVES_OF_CUS=k: at most k x #CUs workgroups (0 = one workgroup per tile, i.e. not
+  // persistent: the dispatcher balances tiles dynamically but each tile pays its pipeline fill)
+  static const int rounds_env = [] {
+    const char* e = std::getenv("LLMT_FGEMM_WAVES_OF_CUS");
+    return e ? std::atoi(e) : 1;
+  }();
+  const long long cap = rounds_env <= 0 ? (long long)a.ntiles : (long long)ncu * rounds_env;
+  a.nwg = (int)(a.ntiles < cap ? a.ntiles : cap);
   static const int debug = [] {
     const char* e = std::getenv("LLMT_FGEMM_DEBUG");
     return e ? std::atoi(e) : 0;

@@ -14,23 +14,27 @@
 // traffic per layer at GPT-2 124M / 64K tokens.  Here those passes ride in the GEMM epilogue.
 //
 // Structure (MI355X playbook: LDS-DMA ring, counted vmcnt + raw barrier, XCD-aware persistent
-// tiles; shared building blocks in gemm_common.h):
-//  * 256x256 output tiles, 4 waves (2x2) of 128x128 = 4x4 v_mfma_f32_32x32x16_bf16 accumulators
-//    (256 fp32 per lane in AGPRs), one 256-thread workgroup per CU;
-//  * PERSISTENT: min(#tiles, #CUs) workgroups; each XCD owns a contiguous range of tiles
-//    (m-major, so the workgroups running together on one XCD share A strips in its L2) and the
-//    32 workgroups of an XCD stride through it.  The K stages of ALL of a workgroup's tiles form
-//    one stream through a 4-slot LDS ring (3 stages in flight), so the next tile's first stages
-//    load while this tile's epilogue runs;
-//  * A image [256 m][32 k] and NT B image [256 n][32 k]: 64-byte rows, 16-byte chunks swizzled
-//    by (row >> 2) & 3 so each ds_read_b128 lane group covers all 64 banks; fragments are
-//    direct 16-byte reads.  NN B image [32 k][256 n] with the wgrad swizzle, read transposed
-//    (ds_read_b64_tr_b16);
+// tiles; shared building blocks in gemm_common.h; measured history in docs/performance.md):
+//  * 256x256 output tiles, 8 waves = two per SIMD: waves 0-3 own the upper 128 rows, waves 4-7
+//    the lower; each wave a 128x64 tile of 8 x 4 v_mfma_f32_16x16x32_bf16 accumulators (128 fp32
+//    per lane), so one wave's LDS reads / waits overlap the other wave's MFMAs on the SIMD;
+//  * PERSISTENT: min(#tiles, #CUs) workgroups; each XCD owns a contiguous range of tiles (raster
+//    in bands of kBand n-tiles, m-major inside a band) and its workgroups stride through it.  The
+//    64-deep K stages of ALL of a workgroup's tiles form one stream through a 2-slot LDS ring
+//    (128 KiB: stage g+1 lands while stage g computes), so the next tile's first stage loads
+//    while this tile's epilogue runs;
+//  * A image [256 m][64 k] and NT B image [256 n][64 k]: 128-byte rows (each 1-KiB LDS-DMA op
+//    moves 8 whole cache lines), 16-byte chunks XOR (row & 7) so every ds_read_b128 lane group of
+//    a 16x16x32 fragment read hits 16 distinct bank slots.  NN B image [64 k][256 n] with the
+//    wgrad swizzle, read transposed (ds_read_b64_tr_b16);
+//  * fragment reads are issued one MFMA sub-group (16 MFMAs) ahead; one wait + barrier per stage,
+//    placed before the last sub-group so the next stage's first fragments load under it;
 //  * MFMA srcA = B fragment, srcB = A fragment, so a lane's accumulator column is one output ROW
-//    and its registers run along N in groups of 4 — the epilogue stages each 32x64 piece through
-//    a per-wave XOR-swizzled fp32 LDS image (no cross-wave sync) and writes 16-byte row
-//    segments with buffer stores (out-of-range lanes get an offset past the descriptor, so the
-//    store count is branch-free and known: the counted waits after an epilogue rely on it).
+//    and its registers run along N in groups of 4 — the epilogue stages each 16x64 piece through
+//    a per-wave XOR-swizzled fp32 LDS image (no cross-wave sync) and writes 16-byte stores, 8
+//    whole 128-byte row segments per wave instruction, with buffer stores (out-of-range lanes get
+//    an offset past the descriptor, so the store count is branch-free and known: the counted
+//    waits after an epilogue rely on it); the tile's bias rides with its last K stage by LDS-DMA.
 #include <cstdlib>
 
 #include "common.h"

@@ -78,7 +78,7 @@ def gemm(M: int = 32768, only: str = "") -> list[dict]:
     return rows
 
 
-def fgemm(M: int = 65536) -> list[dict]:
+def fgemm(M: int = 65536, only: str = "") -> list[dict]:
     """llmtrain fused forward/dX GEMM (csrc/gemm_fused.hip) against hipBLASLt (+ the separate
     GELU kernels it replaces) on the GPT-2 124M shapes."""
     from llmtrain.ops import _ext
@@ -88,6 +88,8 @@ def fgemm(M: int = 65536) -> list[dict]:
     dev = torch.device("cuda")
     rows = []
     shapes = {"qkv": (768, 2304), "out": (768, 768), "fc": (768, 3072), "proj": (3072, 768)}
+    if only == "head":
+        shapes = {"head": (768, 50304)}
     for name, (K, N) in shapes.items():
         x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
         w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) / K**0.5
@@ -207,5 +209,7 @@ if __name__ == "__main__":
                   M=int(sys.argv[6]) if len(sys.argv) > 6 else 65536)
     if what == "fgemm":
         fgemm(int(sys.argv[2]) if len(sys.argv) > 2 else 65536)
+    if what == "fgemm_head":  # LM-head shapes (K 768 fwd, K 50304 dX)
+        fgemm(int(sys.argv[2]) if len(sys.argv) > 2 else 32768, only="head")
     if what in ("attn", "all"):
         attn()

@@ -158,6 +158,7 @@ def main() -> int:
             "alloc_retries": int(torch.cuda.memory_stats().get("num_alloc_retries", 0)),
             "device_mallocs": int(torch.cuda.memory_stats().get("num_device_alloc", 0)),
             "reserved_gib": round(torch.cuda.memory_reserved() / 2**30, 2),
+            "tuned_gemm_table": bool(getattr(trainer, "tuned_gemms", False)),
             "device_free_total_gib": [round(v / 2**30, 1) for v in torch.cuda.mem_get_info()],
         }
         print(json.dumps(result), flush=True)

@@ -152,6 +152,8 @@ def build_parser() -> argparse.ArgumentParser:
     gen.add_argument("--top-next", type=int, default=0, help="Also list the k most likely next tokens.")
     gen.add_argument("--device", default=None, help="Override run.device (cpu | cuda).")
     gen.add_argument("--no-cache", action="store_true", help="Recompute the full context every step.")
+    gen.add_argument("--graph", action="store_true",
+                     help="Decode through a captured hipGraph (one graph launch per token on GPU).")
     return parser
 
 
@@ -329,6 +331,7 @@ def _handle_generate(args: argparse.Namespace) -> int:
             text = generate_text(
                 model, tokenizer, prompt, max_new_tokens=args.max_new_tokens, temperature=args.temperature,
                 top_k=args.top_k if args.top_k > 0 else None, seed=args.seed, use_cache=not args.no_cache,
+                use_graph=args.graph,
             )
             entry: dict[str, Any] = {"prompt": prompt, "completion": text}
             if args.top_next > 0:

@@ -8,5 +8,6 @@ from llmtrain.inference.generate import (
     sample_next_token,
     top_next_tokens,
 )
+from llmtrain.inference.graph_decode import GraphDecoder
 
-__all__ = ["KVCache", "forward_cached", "generate", "generate_text", "sample_next_token", "top_next_tokens"]
+__all__ = ["GraphDecoder", "KVCache", "forward_cached", "generate", "generate_text", "sample_next_token", "top_next_tokens"]

@@ -114,9 +114,12 @@ def generate(
     generator: torch.Generator | None = None,
     use_cache: bool = True,
     autocast_dtype: torch.dtype | None = None,
+    use_graph: bool = False,
 ) -> torch.Tensor:
     """Extend ``ids`` [B, T0] by up to ``max_new_tokens`` sampled tokens (stops early once every
-    row has produced ``eos_token_id``)."""
+    row has produced ``eos_token_id``).  ``use_graph`` decodes through a captured hipGraph
+    (:class:`llmtrain.inference.graph_decode.GraphDecoder`; GPU, weights already in the compute
+    dtype, no autocast); the sampled tokens follow the same RNG stream as the eager path."""
     was_training = model.training
     model.eval()
     device = ids.device
@@ -129,10 +132,21 @@ def generate(
     out = ids
     done = torch.zeros(ids.shape[0], dtype=torch.bool, device=device)
     cache: KVCache | None = None
+    decoder = None
+    if use_graph and use_cache and autocast_dtype is None:
+        from llmtrain.inference.graph_decode import GraphDecoder
+
+        decoder = GraphDecoder.for_model(model, ids.shape[0])  # captured once on GPU; eager static step on CPU
+        decoder.cache.length = 0
     try:
         with ctx:
             for _ in range(max_new_tokens):
-                if use_cache and out.shape[1] <= block:
+                if decoder is not None and out.shape[1] <= block:
+                    if decoder.length == 0:
+                        logits = decoder.prefill(out).clone()
+                    else:
+                        logits = decoder.decode(out[:, -1:]).clone()
+                elif decoder is None and use_cache and out.shape[1] <= block:
                     if cache is None:
                         dtype = model.token_embedding.weight.dtype if autocast_dtype is None else autocast_dtype
                         cache = KVCache.allocate(model, out.shape[0], dtype=dtype, device=device)
@@ -165,12 +179,15 @@ def generate_text(
     seed: int = 1234,
     *,
     use_cache: bool = True,
+    use_graph: bool = False,
 ) -> str:
     """Notebook-compatible helper: seed, encode, generate, decode."""
     torch.manual_seed(seed)
     device = next(model.parameters()).device
     x = torch.tensor([tokenizer.encode(prompt)], dtype=torch.long, device=device)
-    y = generate(model, x, max_new_tokens, temperature=temperature, top_k=top_k, use_cache=use_cache)
+    y = generate(
+        model, x, max_new_tokens, temperature=temperature, top_k=top_k, use_cache=use_cache, use_graph=use_graph
+    )
     return tokenizer.decode(y[0].tolist())
 
 

@@ -44,6 +44,7 @@ from llmtrain.registry import initialize_registries
 from llmtrain.registry.data import get_data_module
 from llmtrain.registry.models import get_model_adapter
 from llmtrain.runtime.device import resolve_policy, seed_everything
+from llmtrain.runtime.tuning import enable_tuned_gemms
 from llmtrain.tracking import NullTracker, Tracker
 from llmtrain.training.checkpoint import CheckpointManager, CheckpointPayload, restore_rng_states
 from llmtrain.training.optim import FusedAdamW, build_optimizer, fused_clip_coef
@@ -151,6 +152,7 @@ class Trainer:
             policy = dataclasses.replace(policy, use_fused=False)
         self._policy = policy
         self._device = self._policy.device
+        self.tuned_gemms = enable_tuned_gemms(self._device)  # shipped hipBLASLt solution table (GPU)
         model = model.to(self._device)
         if self._policy.use_fused:
             model.prepare_runtime(compute_dtype=self._policy.compute_dtype)

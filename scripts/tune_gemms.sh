@@ -1,0 +1,28 @@
+#!/usr/bin/env bash
+# Tune every hipBLASLt/rocBLAS GEMM the bench issues with PyTorch TunableOp, starting from the
+# shipped table (llmtrain/runtime/tuned/), then (AB=1) A/B the bench with and without the table on
+# the same box.  New table: gpurun_out/tunableop/tuned0.csv (copy it over the shipped one).
+#   BENCH_ARGS="--model gpt2-xl --micro-batch 16 --grad-accum 2" AB=0 bash scripts/tune_gemms.sh
+set -euo pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/tunableop
+mkdir -p "$OUT"
+MB=${MB:-128}
+cp llmtrain/runtime/tuned/gemm_tunableop_gfx950.csv "$OUT/tuned0.csv"
+# 1) tuning pass: every (op, shape) not yet in the table is benchmarked over all library solutions
+PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_VERBOSE=${VERBOSE:-1} \
+PYTORCH_TUNABLEOP_FILENAME="$OUT/tuned.csv" \
+  timeout -k 10 900 python bench.py --steps 1 --warmup 1 --micro-batch "$MB" ${BENCH_ARGS:-} \
+  > "$OUT/tune.log" 2>&1 || { echo "tuning failed"; tail -30 "$OUT/tune.log"; exit 1; }
+cat "$OUT"/tuned0.csv
+[ "${AB:-1}" = 1 ] || exit 0
+# 2) same-box A/B: library heuristics vs the tuned table (tuning off, look-ups only)
+for round in 1 2; do
+  for tag in base tuned; do
+    if [ "$tag" = tuned ]; then envs="PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=0 PYTORCH_TUNABLEOP_FILENAME=$OUT/tuned.csv"; else envs="LLMTRAIN_TUNED_GEMMS=0"; fi
+    env $envs timeout -k 10 300 python bench.py --steps 20 --warmup 5 --micro-batch "$MB" ${BENCH_ARGS:-} \
+      > "$OUT/bench_${tag}_${round}.log" 2>&1 || { echo "bench $tag failed"; tail -20 "$OUT/bench_${tag}_${round}.log"; exit 1; }
+    echo "$tag round$round: $(tail -1 "$OUT/bench_${tag}_${round}.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
+  done
+done

@@ -124,3 +124,33 @@ def test_cached_decode_on_gpu(gpu_device) -> None:  # type: ignore[no-untyped-de
         torch.testing.assert_close(got, want, rtol=1e-3, atol=1e-3)
     out = generate(model, ids[:, :8], 70, temperature=0.9, top_k=20, autocast_dtype=torch.bfloat16)
     assert out.shape == (3, 78) and int(out.max()) < 512
+
+
+def test_graph_decoder_static_step_matches_full_forward() -> None:
+    """The static-shape step the hipGraph records (full-capacity masked attention, device-side
+    position) equals the full forward at every position, here run eagerly on CPU."""
+    from llmtrain.inference import GraphDecoder
+
+    model = _model(block=16)
+    ids = torch.randint(0, 64, (3, 16))
+    dec = GraphDecoder(model, 3)
+    assert not dec.use_graph
+    logits = dec.prefill(ids[:, :5])
+    torch.testing.assert_close(logits, model(ids[:, :5])[:, -1], rtol=1e-10, atol=1e-10)
+    for t in range(5, 16):
+        logits = dec.decode(ids[:, t : t + 1])
+        torch.testing.assert_close(logits, model(ids[:, : t + 1])[:, -1], rtol=1e-10, atol=1e-10)
+    assert dec.length == 16
+    with pytest.raises(ValueError, match="full"):
+        dec.decode(ids[:, :1])
+
+
+@pytest.mark.parametrize("temperature,top_k", [(0.0, None), (0.9, 8)])
+def test_generate_graph_path_matches_cached_path(temperature: float, top_k: int | None) -> None:
+    model = _model(block=16)
+    prompt = torch.randint(0, 64, (2, 4))
+    torch.manual_seed(11)
+    want = generate(model, prompt, 18, temperature=temperature, top_k=top_k)  # crosses block_size
+    torch.manual_seed(11)
+    got = generate(model, prompt, 18, temperature=temperature, top_k=top_k, use_graph=True)
+    assert torch.equal(got, want)

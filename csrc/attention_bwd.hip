@@ -33,10 +33,14 @@ constexpr int kBwdWaves = 8;
 constexpr int kKvBlk = 32 * kBwdWaves;  // 256 keys per workgroup
 constexpr int kQTile = 64;  // query rows per sweep step (two 32-row MFMA tiles)
 
-// delta[b, h, t] = sum_d dO[b, t, h, d] * O[b, t, h, d]; a workgroup owns 32 consecutive t of one
-// (b, h), 8 lanes per row.  With `dbias_v` it also accumulates the column sums of dO per head:
+// delta[b, h, t] = sum_d dO[b, t, h, d] * O[b, t, h, d]; a workgroup owns kDeltaRows consecutive t
+// of one (b, h) in kDeltaRows / 32 unrolled sweeps of 32 rows (8 lanes per row, every sweep's
+// loads issued up front).  With `dbias_v` it also accumulates the column sums of dO per head:
 // without dropout every valid row of P sums to 1, so sum_key dV[key, d] = sum_q dO[q, d] — the
 // V part of the qkv-bias gradient costs one LDS reduction here instead of a pass over dqkv.
+// 256 rows per workgroup keep the float atomics at 64 per 256 rows: with 32-row workgroups the
+// 64 addresses of a head took B*T/32 atomics each and the kernel ran at 1.8 TB/s.
+constexpr int kDeltaRows = 256;
 __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restrict__ dout,
                                                          const bf16_raw* __restrict__ out,
                                                          float* __restrict__ delta, float* __restrict__ dbias_v,
@@ -45,33 +49,49 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
   const int bh = blockIdx.y;
   const int b = bh / H, h = bh - b * H;
   const int rl = threadIdx.x >> 3, sub = threadIdx.x & 7;
-  const int t = blockIdx.x * 32 + rl;
-  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  float acc = 0.f;
-  if (t < T) {
-    const long row = ((long)b * T + t) * H + h;
-    float o[8];
-    unpack8(*reinterpret_cast<const ushort8_t*>(dout + row * kHD + 8 * sub), a);
-    unpack8(*reinterpret_cast<const ushort8_t*>(out + row * kHD + 8 * sub), o);
+  constexpr int kSweeps = kDeltaRows / 32;
+  ushort8_t dv[kSweeps], ov[kSweeps];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc += a[i] * o[i];
+  for (int it = 0; it < kSweeps; ++it) {
+    const int t = blockIdx.x * kDeltaRows + 32 * it + rl;
+    dv[it] = ushort8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    ov[it] = dv[it];
+    if (t < T) {
+      const long row = ((long)b * T + t) * H + h;
+      dv[it] = *reinterpret_cast<const ushort8_t*>(dout + row * kHD + 8 * sub);
+      ov[it] = *reinterpret_cast<const ushort8_t*>(out + row * kHD + 8 * sub);
+    }
   }
-  acc += __shfl_xor(acc, 1, 64);
-  acc += __shfl_xor(acc, 2, 64);
-  acc += __shfl_xor(acc, 4, 64);
-  if (t < T && sub == 0) delta[(long)bh * T + t] = acc;
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < kSweeps; ++it) {
+    float a[8], o[8];
+    unpack8(dv[it], a);
+    unpack8(ov[it], o);
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      acc += a[i] * o[i];
+      csum[i] += a[i];  // rows past T loaded as zeros
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    const int t = blockIdx.x * kDeltaRows + 32 * it + rl;
+    if (t < T && sub == 0) delta[(long)bh * T + t] = acc;
+  }
   if (dbias_v == nullptr) return;  // uniform: kernel argument
   // column sums: over the wave's 8 rows with shuffles (lanes sharing `sub`), then the 4 waves
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    a[i] += __shfl_xor(a[i], 8, 64);
-    a[i] += __shfl_xor(a[i], 16, 64);
-    a[i] += __shfl_xor(a[i], 32, 64);
+    csum[i] += __shfl_xor(csum[i], 8, 64);
+    csum[i] += __shfl_xor(csum[i], 16, 64);
+    csum[i] += __shfl_xor(csum[i], 32, 64);
   }
   const int wv = threadIdx.x >> 6;
   if ((threadIdx.x & 63) < 8) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) red[wv][8 * sub + i] = a[i];
+    for (int i = 0; i < 8; ++i) red[wv][8 * sub + i] = csum[i];
   }
   __syncthreads();
   if (threadIdx.x < kHD) {
@@ -82,50 +102,67 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
 
 // dqkv[b, t, 0, h, :] = bf16(sum over key blocks kb <= t / 256 of dq_part[kb][b, h, t, :]):
 // the main kernel stores each key block's dQ contribution with plain stores (no memset, no
-// atomics); rows only ever read the partials their causal key blocks wrote.
+// atomics); rows only ever read the partials their causal key blocks wrote.  A workgroup owns
+// kDqRows rows t of one (b, h) inside one 256-key block, so all its rows sum the same number of
+// planes; row tiles are dispatched last-first (most planes first) and the Q part of the qkv-bias
+// gradient (column sums of dQ) leaves the workgroup as 64 atomics per kDqRows rows.
+constexpr int kDqRows = 64;
 __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const float* __restrict__ part, bf16_raw* __restrict__ dqkv,
-                                                             float* __restrict__ dbias, int T, int H, int nkb, long n8) {
-  __shared__ float red[32][65];  // [row in block][d] for the Q-bias column sums
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // one 8-element chunk
-  const long row = i >> 3;  // (b*H + h)*T + t
-  const int c = (int)(i & 7);
-  const long bh = row / T;
-  const int t = (int)(row - bh * T);
-  const long b = bh / H;
-  const int h = (int)(bh - b * H);
-  float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (i < n8) {
-    const long plane = n8 * 8;  // floats per key-block partial
-    const int last = min(t / kKvBlk, nkb - 1);
-    for (int kb = 0; kb <= last; ++kb) {
-      const float4_t* src = reinterpret_cast<const float4_t*>(part + kb * plane + row * kHD + 8 * c);
+                                                             float* __restrict__ dbias, int T, int H, int nkb, long plane) {
+  __shared__ float red[4][kHD];
+  const int bh = blockIdx.x;
+  const int b = bh / H, h = bh - b * H;
+  const int rl = threadIdx.x >> 3, c = threadIdx.x & 7;
+  const int tile = (int)(gridDim.y - 1 - blockIdx.y);  // heavy (late) rows first
+  const int t0 = tile * kDqRows + rl;  // this thread's rows: t0 + 32 * it
+  const int last = min(tile * kDqRows / kKvBlk, nkb - 1);
+  constexpr int kSweeps = kDqRows / 32;
+  // key-block planes outermost: each plane step issues all 16 loads of the thread's 8 rows at
+  // once (rows past T re-read row T - 1, which every plane up to `last` holds; result unused)
+  float f[kSweeps][8];
+#pragma unroll
+  for (int it = 0; it < kSweeps; ++it)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[it][j] = 0.f;
+  for (int kb = 0; kb <= last; ++kb) {
+#pragma unroll
+    for (int it = 0; it < kSweeps; ++it) {
+      const int t = min(t0 + 32 * it, T - 1);
+      const float4_t* src = reinterpret_cast<const float4_t*>(part + kb * plane + ((long)bh * T + t) * kHD + 8 * c);
       const float4_t x = src[0], y = src[1];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        f[j] += x[j];
-        f[4 + j] += y[j];
+        f[it][j] += x[j];
+        f[it][4 + j] += y[j];
       }
     }
-    *reinterpret_cast<ushort8_t*>(dqkv + ((b * T + t) * 3L * H + h) * kHD + 8 * c) = pack8(f);
+  }
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < kSweeps; ++it) {
+    const int t = t0 + 32 * it;
+    if (t < T) {
+      *reinterpret_cast<ushort8_t*>(dqkv + (((long)b * T + t) * 3L * H + h) * kHD + 8 * c) = pack8(f[it]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) csum[j] += f[it][j];
+    }
   }
   if (dbias == nullptr) return;  // uniform: kernel argument
-  // Q part of the qkv-bias gradient: sum this block's 32 rows per head column
-  const long row0 = ((long)blockIdx.x * blockDim.x) >> 3;
-  const long last_row = min(row0 + 31, n8 / 8 - 1);
-  if (row0 / T == last_row / T) {  // the block's rows share one (b, h): LDS reduction, 64 atomics
-    const int rl = threadIdx.x >> 3;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) red[rl][8 * c + j] = f[j];
-    __syncthreads();
-    if (threadIdx.x < 64) {
-      float acc = 0.f;
-      for (int r = 0; r < 32; ++r) acc += red[r][threadIdx.x];
-      const int hh = (int)((row0 / T) % H);
-      atomicAdd(dbias + hh * kHD + threadIdx.x, acc);
-    }
-  } else if (i < n8) {
+  for (int j = 0; j < 8; ++j) {
+    csum[j] += __shfl_xor(csum[j], 8, 64);
+    csum[j] += __shfl_xor(csum[j], 16, 64);
+    csum[j] += __shfl_xor(csum[j], 32, 64);
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) < 8) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) atomicAdd(dbias + h * kHD + 8 * c + j, f[j]);
+    for (int j = 0; j < 8; ++j) red[wv][8 * c + j] = csum[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < kHD) {
+    const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(dbias + h * kHD + threadIdx.x, s);
   }
 }
 
@@ -432,7 +469,7 @@ hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, c
                            DropoutArgs dropout, hipStream_t stream) {
   if (B <= 0 || T <= 0 || H <= 0 || T > 65535) return hipErrorInvalidValue;
   const long rows = (long)B * T * H;
-  hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((T + 31) / 32, B * H), dim3(256), 0, stream,
+  hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((T + attn::kDeltaRows - 1) / attn::kDeltaRows, B * H), dim3(256), 0, stream,
                      (const bf16_raw*)dout, (const bf16_raw*)out, delta,
                      dropout.thr == 0 && dbias != nullptr ? dbias + 2L * H * attn::kHD : nullptr, T, H);
   const int nkb = (T + attn::kKvBlk - 1) / attn::kKvBlk;
@@ -444,9 +481,9 @@ hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, c
     hipLaunchKernelGGL(attn::attn_bwd_kernel<false>, dim3(B * H, nkb), dim3(512), 0, stream, (const bf16_raw*)qkv,
                        (const bf16_raw*)dout, lse, delta, (bf16_raw*)dqkv, dq_part, dbias, T, H, nkb,
                        dropout);
-  const long n8 = rows * attn::kHD / 8;
-  hipLaunchKernelGGL(attn::attn_dq_reduce_kernel, dim3((n8 + 255) / 256), dim3(256), 0, stream, dq_part,
-                     (bf16_raw*)dqkv, dbias, T, H, nkb, n8);
+  hipLaunchKernelGGL(attn::attn_dq_reduce_kernel, dim3(B * H, (T + attn::kDqRows - 1) / attn::kDqRows), dim3(256), 0,
+                     stream, dq_part,
+                     (bf16_raw*)dqkv, dbias, T, H, nkb, rows * (long)attn::kHD);
   return hipGetLastError();
 }
 

@@ -145,14 +145,20 @@ def attn_bwd(dout, qkv, out, lse, bsz: int, seqlen: int, n_heads: int, dropout=(
 # workgroups start late on CUs still draining the previous kernel.  Above this many A bytes the
 # engine stays on hipBLASLt.
 FGEMM_MAX_A_BYTES = int(os.environ.get("LLMTRAIN_FGEMM_MAX_A_MB", "64")) * 2**20
+# Ops that take the fused GEMM at any A size (knob values: fwd, fwd_gelu, dx, dx_gelu).  Default
+# dx_gelu: the MLP-projection dX with GELU backward + fc-bias grad in the epilogue replaces a
+# hipBLASLt GEMM plus a full [M, 4d] read-modify pass, and wins in the whole 124M step too
+# (same-box, micro-batch 128: +0.9 %, 994.9k/995.5k vs 985.8k/986.8k tok/s); adding the plain dX
+# GEMMs (-0.4 %) or the forward GEMMs (-1.6 %) at this size loses (scripts/abn.sh).
+FGEMM_ANY_SIZE = frozenset(filter(None, os.environ.get("LLMTRAIN_FGEMM_ANY_SIZE", "dx_gelu").split(",")))
 
 
-def _fgemm_ok(a: torch.Tensor, k: int, n: int, *others: torch.Tensor | None) -> bool:
+def _fgemm_ok(a: torch.Tensor, k: int, n: int, *others: torch.Tensor | None, op: str = "") -> bool:
     """Shapes/placements the fused MFMA GEMM (csrc/gemm_fused.hip) takes and wins on:
     K % 64 == 0, K >= 256, N % 8 == 0, 16-byte aligned operands, A small enough (see above)."""
     if not (k % 64 == 0 and k >= 256 and n % 8 == 0):
         return False
-    if a.numel() * a.element_size() > FGEMM_MAX_A_BYTES:
+    if a.numel() * a.element_size() > FGEMM_MAX_A_BYTES and op not in FGEMM_ANY_SIZE:
         return False
     return all(t is None or t.data_ptr() % 16 == 0 for t in (a, *others))
 
@@ -160,7 +166,7 @@ def _fgemm_ok(a: torch.Tensor, k: int, n: int, *others: torch.Tensor | None) -> 
 def linear_fwd(x, w, bias=None):
     """``x @ w^T + bias`` (nn.Linear forward, bf16 out).  GPU: the fused MFMA GEMM with the bias in
     its epilogue where the shape allows, else hipBLASLt."""
-    if _on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x, x.shape[1], w.shape[0], w, bias):
+    if _on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x, x.shape[1], w.shape[0], w, bias, op="fwd"):
         return hip_ops().gemm_fused(x, w, False, 0, bias)[0]
     return torch.mm(x, w.t()) if bias is None else torch.addmm(bias, x, w.t())
 
@@ -168,7 +174,7 @@ def linear_fwd(x, w, bias=None):
 def linear_fwd_gelu(x, w, bias=None):
     """``u = x @ w^T + bias`` and ``g = gelu(u)`` (exact erf GELU of the bf16 ``u``, which the
     backward reads): on GPU the GELU rides in the GEMM epilogue, no separate pass over ``u``."""
-    if _on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x, x.shape[1], w.shape[0], w, bias):
+    if _on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x, x.shape[1], w.shape[0], w, bias, op="fwd_gelu"):
         u, g = hip_ops().gemm_fused(x, w, False, 1, bias)
         return u, g
     u = torch.mm(x, w.t()) if bias is None else torch.addmm(bias, x, w.t())
@@ -177,7 +183,7 @@ def linear_fwd_gelu(x, w, bias=None):
 
 def linear_dx(dy, w):
     """``dy @ w`` (data gradient of nn.Linear with weight ``w [out, in]``)."""
-    if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy, dy.shape[1], w.shape[1], w):
+    if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy, dy.shape[1], w.shape[1], w, op="dx"):
         return hip_ops().gemm_fused(dy, w, True, 0)[0]
     return torch.mm(dy, w)
 
@@ -186,7 +192,7 @@ def linear_dx_gelu_bwd(dy, w, u, dbias=None):
     """``du = (dy @ w) * gelu'(u)`` and ``dbias += colsum(du)``: the data gradient of the MLP
     projection fused with the GELU backward and the fc bias gradient (one GEMM epilogue on GPU
     instead of a GEMM plus a full read-modify pass over the [M, d_ff] activations)."""
-    if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy, dy.shape[1], w.shape[1], w, u):
+    if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy, dy.shape[1], w.shape[1], w, u, op="dx_gelu"):
         return hip_ops().gemm_fused(dy, w, True, 2, None, u, dbias)[0]
     return gelu_bwd(torch.mm(dy, w), u, dbias)
 

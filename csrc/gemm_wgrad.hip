@@ -170,7 +170,7 @@ struct Plan {
 
 // Modelled time of one configuration: rounds of workgroups x per-workgroup MFMA time at the
 // tile's measured efficiency, plus the split-K atomic traffic at the chip-wide atomic rate.
-Plan plan_for(int tile, int M, int N, int K, int split_req, int ncu) {
+Plan plan_for(int tile, int M, int N, int K, int split_req, int ncu, int min_split) {
   Plan p;
   p.tile = tile;
   const int bn = tile, bk = tile;
@@ -198,10 +198,11 @@ Plan plan_for(int tile, int M, int N, int K, int split_req, int ncu) {
     }
   };
   if (split_req > 0) {
-    eval(split_req < max_split ? split_req : max_split, p);
+    const int s = split_req > min_split ? split_req : min_split;
+    eval(s < max_split ? s : max_split, p);
   } else {
     const int hi = max_split < 4 * slots ? max_split : 4 * slots;
-    for (int s = 1; s <= hi; ++s) eval(s, p);
+    for (int s = min_split; s <= (hi > min_split ? hi : min_split); ++s) eval(s, p);
   }
   return p;
 }
@@ -211,7 +212,9 @@ Plan plan_for(int tile, int M, int N, int K, int split_req, int ncu) {
 hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N,
                              int K, int split, int tile, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return hipSuccess;
-  if (lda % 8 || ldb % 8 || N % 8 || K % 8) return hipErrorInvalidValue;
+  // N needs no alignment: tiles past N read the next rows' data (or zeros past the chunk) into
+  // accumulators whose atomics the epilogue masks with n < N (the LM head's N = 50257)
+  if (lda % 8 || ldb % 8 || K % 8 || lda < N) return hipErrorInvalidValue;
   if (tile == 0) {
     static const int forced = [] {
       const char* e = std::getenv("LLMT_WGRAD_TILE");
@@ -226,12 +229,16 @@ hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, fl
     return e ? std::atoi(e) : 0;
   }();
   const int ncu = cus_env > 0 ? cus_env : gemm::cu_count();
+  // 32-bit buffer offsets: one M chunk of either operand must stay below 2 GiB (wide rows such
+  // as the LM head's 50304-column logits force a minimum split)
+  const long long row_bytes = 2LL * (lda > ldb ? lda : ldb);
+  const int min_split = (int)(((long long)M * row_bytes + (1LL << 31) - 1 - 4096) / ((1LL << 31) - 4096 - row_bytes * 32));
   wgrad::Plan p;
   if (tile == 128 || tile == 256) {
-    p = wgrad::plan_for(tile, M, N, K, split, ncu);
+    p = wgrad::plan_for(tile, M, N, K, split, ncu, min_split > 0 ? min_split : 1);
   } else {
-    const wgrad::Plan a = wgrad::plan_for(256, M, N, K, split, ncu);
-    const wgrad::Plan b = wgrad::plan_for(128, M, N, K, split, ncu);
+    const wgrad::Plan a = wgrad::plan_for(256, M, N, K, split, ncu, min_split > 0 ? min_split : 1);
+    const wgrad::Plan b = wgrad::plan_for(128, M, N, K, split, ncu, min_split > 0 ? min_split : 1);
     p = a.cost <= b.cost ? a : b;
   }
   // 32-bit buffer offsets: one chunk of either operand must stay below 2 GiB

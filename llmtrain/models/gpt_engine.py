@@ -397,6 +397,11 @@ class FusedGPTEngine:
             with torch.cuda.stream(side):
                 accumulate_wgrad(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled)
             held = (dlogits, hf_scaled)
+        elif dlogits.is_cuda and dlogits.dtype == torch.bfloat16:
+            # split-K MFMA kernel: 9.78 vs 10.34 ms for hipBLASLt's fp32-output GEMM at 128K tokens
+            # (bench/head_wgrad.py; N = 50257 rows inside the 50304-wide padded logits)
+            self._wgrad_now(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled)
+            held = None
         else:
             accumulate_wgrad(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled)
             held = None

@@ -201,7 +201,8 @@ def test_attention_causality(gpu_device):
 
 @pytest.mark.parametrize("tile", [0, 128, 256])
 @pytest.mark.parametrize("M,N,K,lda", [(4096, 768, 768, 768), (2048, 2304, 768, 2304), (1000, 200, 72, 200),
-                                        (3000, 1000, 768, 1024), (2080, 1600, 4800, 1600)])
+                                        (3000, 1000, 768, 1024), (2080, 1600, 4800, 1600),
+                                        (1500, 1001, 768, 1024)])  # odd N in a padded row (LM head)
 def test_wgrad_gemm(gpu_device, M, N, K, lda, tile):
     """Split-K MFMA weight-gradient GEMM accumulates dY^T X into an existing fp32 buffer, for both
     tile configurations and the cost-model choice; also with a column-slice dY (row stride

@@ -48,7 +48,8 @@ def make_config(args: argparse.Namespace, world: int):
         "data": {
             "name": "synthetic_tokens",
             "num_workers": 0,
-            "extra": {"train_sequences": max(256, 4 * args.micro_batch), "val_sequences": 0},
+            # every rank's DistributedSampler shard must hold whole micro-batches (8 ranks x 128)
+            "extra": {"train_sequences": max(256, 4 * args.micro_batch * args.grad_accum * world), "val_sequences": 0},
         },
         "trainer": {
             "max_steps": args.warmup + args.steps + 1,
@@ -113,6 +114,9 @@ def main() -> int:
     barrier()
     elapsed = time.perf_counter() - t0
     final_loss = float(loss.item())
+    want = args.steps * cfg.trainer.micro_batch_size * cfg.trainer.grad_accum_steps * cfg.model.block_size
+    if tokens != want:  # a short data shard would silently shrink the per-GPU batch
+        raise RuntimeError(f"rank {rank}: timed {tokens} tokens, expected {want}")
 
     elapsed_t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     tokens_t = torch.tensor([tokens], dtype=torch.float64, device="cuda")

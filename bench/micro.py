@@ -203,7 +203,7 @@ if __name__ == "__main__":
     if what == "fwd":  # forward / dX GEMMs
         gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 65536, only="fwd")
     if what == "ln":
-        ln()
+        ln(int(sys.argv[2]) if len(sys.argv) > 2 else 65536)
     if what == "fgemm1":  # K N epi b_kn
         fgemm_one(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5] == "1",
                   M=int(sys.argv[6]) if len(sys.argv) > 6 else 65536)

@@ -102,6 +102,21 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
 
 constexpr int kBwdWaves = 4;
 
+// Raw (unconverted) row chunk: the next row's operands are prefetched into these registers while
+// the current row is reduced, so every wave keeps two rows of loads in flight (the reductions
+// and the dependent stores otherwise serialise one HBM round trip per row).
+template <typename T> struct Raw4;
+template <> struct Raw4<float> { typedef float4_t type; };
+template <> struct Raw4<bf16_raw> { typedef ushort4_t type; };
+template <typename T>
+__device__ __forceinline__ typename Raw4<T>::type load_raw4(const T* p) {
+  return *reinterpret_cast<const typename Raw4<T>::type*>(p);
+}
+__device__ __forceinline__ float4_t to_f4(float4_t v) { return v; }
+__device__ __forceinline__ float4_t to_f4(ushort4_t v) {
+  return float4_t{bf2f(v[0]), bf2f(v[1]), bf2f(v[2]), bf2f(v[3])};
+}
+
 template <int MAXC, typename TDY, bool LOWP_OUT>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const TDY* __restrict__ dy, const float* __restrict__ xs, const float* __restrict__ mean,
@@ -109,10 +124,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const float* __restrict__ dy_scale, float* __restrict__ dx, TDY* __restrict__ dx_lp,
     float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dproj, int M, int d, DropoutArgs dr) {
   extern __shared__ __attribute__((aligned(16))) float smem[];  // [kBwdWaves][d], reused per accumulator
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nc = d >> 2;
   const float scale = dy_scale != nullptr ? *dy_scale : 1.f;
   const float inv_d = 1.f / (float)d;
+  // prefetching doubles the live operand registers: only for rows of <= 768 columns
+  constexpr bool kPrefetch = MAXC <= 3;
 
   float4_t pw[MAXC], pb[MAXC], pp[MAXC];
   float4_t wv[MAXC];
@@ -124,16 +141,74 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 
   const long stride = (long)gridDim.x * kBwdWaves;
-  for (long row = (long)blockIdx.x * kBwdWaves + wid; row < M; row += stride) {
-    const float mu = mean[row], rs = rstd[row];
-    float4_t g[MAXC], xh[MAXC];
+  long row = (long)blockIdx.x * kBwdWaves + wid;
+  typename Raw4<TDY>::type ng[MAXC];
+  float4_t nx[MAXC];
+  float nmu = 0.f, nrs = 0.f;
+  if (kPrefetch && row < M) {
+    nmu = mean[row];
+    nrs = rstd[row];
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = lane + j * 64;
+      if (c < nc) {
+        ng[j] = load_raw4(dy + row * d + 4 * c);
+        nx[j] = load_raw4(xs + row * d + 4 * c);
+      }
+    }
+  }
+  for (; row < M; row += stride) {
+    float mu, rs;
+    float4_t g[MAXC], xh[MAXC], rr[MAXC];
+    if (kPrefetch) {
+      mu = nmu;
+      rs = nrs;
+#pragma unroll
+      for (int j = 0; j < MAXC; ++j) {
+        g[j] = to_f4(ng[j]);
+        xh[j] = nx[j];
+      }
+    } else {
+      mu = mean[row];
+      rs = rstd[row];
+#pragma unroll
+      for (int j = 0; j < MAXC; ++j) {
+        const int c = lane + j * 64;
+        if (c < nc) {
+          g[j] = load4(dy + row * d + 4 * c);
+          xh[j] = load4(xs + row * d + 4 * c);
+        }
+      }
+    }
+    if (dresid != nullptr) {
+#pragma unroll
+      for (int j = 0; j < MAXC; ++j) {
+        const int c = lane + j * 64;
+        if (c < nc) rr[j] = load4(dresid + row * d + 4 * c);
+      }
+    }
+    if (kPrefetch) {
+      const long nrow = row + stride;
+      if (nrow < M) {
+        nmu = mean[nrow];
+        nrs = rstd[nrow];
+#pragma unroll
+        for (int j = 0; j < MAXC; ++j) {
+          const int c = lane + j * 64;
+          if (c < nc) {
+            ng[j] = load_raw4(dy + nrow * d + 4 * c);
+            nx[j] = load_raw4(xs + nrow * d + 4 * c);
+          }
+        }
+      }
+    }
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
       const int c = lane + j * 64;
       if (c < nc) {
-        g[j] = load4(dy + row * d + 4 * c) * scale;
-        xh[j] = (load4(xs + row * d + 4 * c) - mu) * rs;
+        g[j] = g[j] * scale;
+        xh[j] = (xh[j] - mu) * rs;
         float4_t gw = g[j] * wv[j];
         s1 += gw[0] + gw[1] + gw[2] + gw[3];
         float4_t gx = gw * xh[j];
@@ -146,7 +221,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       const int c = lane + j * 64;
       if (c < nc) {
         float4_t out = (g[j] * wv[j] - c1 - xh[j] * c2) * rs;
-        if (dresid != nullptr) out += load4(dresid + row * d + 4 * c);
+        if (dresid != nullptr) out += rr[j];
         store4(dx + row * d + 4 * c, out);
         // the branch that fed this residual stream sees its dropout mask (forward: add_ln_fwd)
         float4_t br = out;
@@ -204,8 +279,24 @@ void launch_fwd_c(const LnFwdArgs& a, hipStream_t st) {
 
 template <int MAXC>
 void launch_bwd_c(const LnBwdArgs& a, hipStream_t st) {
-  const int grid = stride_grid((long long)(a.M + kBwdWaves - 1) / kBwdWaves, 1, 256 * 4);
   const size_t shm = (size_t)kBwdWaves * a.d * sizeof(float);
+  // exactly one resident wave of workgroups (a second partial wave would be a pure tail: every
+  // workgroup runs the same number of rows)
+  static int resident[2][2] = {{0, 0}, {0, 0}};
+  int& per_cu = resident[a.dy_bf16 ? 1 : 0][a.dx_lp != nullptr ? 1 : 0];
+  if (per_cu == 0) {
+    int n = 0, dev = 0, cus = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (a.dy_bf16)
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, a.dx_lp ? ln_bwd_kernel<MAXC, bf16_raw, true>
+                                                              : ln_bwd_kernel<MAXC, bf16_raw, false>, 256, shm);
+    else
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, a.dx_lp ? ln_bwd_kernel<MAXC, float, true>
+                                                              : ln_bwd_kernel<MAXC, float, false>, 256, shm);
+    per_cu = (n > 0 ? n : 4) * (cus > 0 ? cus : 256);
+  }
+  const int grid = stride_grid((long long)(a.M + kBwdWaves - 1) / kBwdWaves, 1, per_cu);
 #define LN_BWD(TDY, LP)                                                                         \
   hipLaunchKernelGGL((ln_bwd_kernel<MAXC, TDY, LP>), dim3(grid), dim3(256), shm, st,            \
                      (const TDY*)a.dy, a.xs, a.mean, a.rstd, a.w, a.dresid, a.dy_scale, a.dx,    \

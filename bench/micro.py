@@ -212,4 +212,4 @@ if __name__ == "__main__":
     if what == "fgemm_head":  # LM-head shapes (K 768 fwd, K 50304 dX)
         fgemm(int(sys.argv[2]) if len(sys.argv) > 2 else 32768, only="head")
     if what in ("attn", "all"):
-        attn()
+        attn(int(sys.argv[2]) if what == "attn" and len(sys.argv) > 2 else 32)

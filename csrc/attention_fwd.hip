@@ -142,9 +142,20 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
 #pragma unroll
         for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, s[kt][r]);
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float m_new = fmaxf(m_run, tmax);  // raw-score units
-      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
-      const float mc = m_new * c;
+      // lazy rescale: keep a stale running max while no row's max grew by more than 2^8 in
+      // probability (P <= 256 is exact enough in fp32 and bf16; l and O use the same stale max,
+      // so the result is unchanged).  The O/l rescale (16 packed muls + one exp per lane) then
+      // runs only on the few tiles where some row of the wave jumps, wave-uniformly.  The first
+      // tile always rescales (m_run = -inf), and tile 0 gives every row a finite max.
+      if (__builtin_amdgcn_ballot_w64((tmax - m_run) * c > 8.f) != 0) {
+        const float m_new = fmaxf(m_run, tmax);  // raw-score units
+        const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
+        l_run *= alpha;
+        o[0] *= alpha;
+        o[1] *= alpha;
+        m_run = m_new;
+      }
+      const float mc = m_run * c;
       float psum = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
@@ -166,10 +177,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
             s[kt][r] = drop_keep(pseed, dr.thr, e) ? s[kt][r] * dr.scale : 0.f;
           }
       }
-      l_run = l_run * alpha + psum;
-      m_run = m_new;
-      o[0] *= alpha;
-      o[1] *= alpha;
+      l_run += psum;
       // O^T += V^T P^T: P^T (the S^T accumulator) is the B operand straight from registers
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {

@@ -466,10 +466,11 @@ long attn_bwd_workspace_floats(int B, int T, int H) {
 
 hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse, void* dqkv,
                            float* delta, float* dq_part, float* dbias, int B, int T, int H,
-                           DropoutArgs dropout, hipStream_t stream) {
+                           DropoutArgs dropout, hipStream_t stream, bool delta_ready) {
   if (B <= 0 || T <= 0 || H <= 0 || T > 65535) return hipErrorInvalidValue;
   const long rows = (long)B * T * H;
-  hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((T + attn::kDeltaRows - 1) / attn::kDeltaRows, B * H), dim3(256), 0, stream,
+  if (!delta_ready)
+    hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((T + attn::kDeltaRows - 1) / attn::kDeltaRows, B * H), dim3(256), 0, stream,
                      (const bf16_raw*)dout, (const bf16_raw*)out, delta,
                      dropout.thr == 0 && dbias != nullptr ? dbias + 2L * H * attn::kHD : nullptr, T, H);
   const int nkb = (T + attn::kKvBlk - 1) / attn::kKvBlk;

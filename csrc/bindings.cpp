@@ -286,7 +286,8 @@ std::tuple<Tensor, Tensor> attn_fwd(const Tensor& qkv, int64_t B, int64_t T, int
 }
 
 Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const Tensor& lse, int64_t B, int64_t T,
-                int64_t H, double dropout_p, int64_t dropout_seed, const c10::optional<Tensor>& dbias) {
+                int64_t H, double dropout_p, int64_t dropout_seed, const c10::optional<Tensor>& dbias,
+                const c10::optional<Tensor>& delta_in) {
   check_qkv(qkv, B, T, H);
   for (const Tensor* t : {&dout, &out}) {
     check_gpu(*t, "dout/out");
@@ -298,7 +299,16 @@ Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const 
   TORCH_CHECK(lse.numel() == B * H * T, "lse must be [B, H, T]");
   at::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
   Tensor dqkv = at::empty_like(qkv);
-  Tensor delta = at::empty({B, H, T}, lse.options());
+  // delta_in: rowsum(dO * O) from the out-proj dX GEMM's epilogue (gemm_fused epilogue 3)
+  Tensor delta;
+  if (delta_in.has_value()) {
+    check_gpu(*delta_in, "delta");
+    check_dtype(*delta_in, at::kFloat, "delta");
+    TORCH_CHECK(delta_in->numel() == B * H * T && delta_in->is_contiguous(), "delta must be [B, H, T]");
+    delta = *delta_in;
+  } else {
+    delta = at::empty({B, H, T}, lse.options());
+  }
   Tensor dq = at::empty({llmt::attn_bwd_workspace_floats((int)B, (int)T, (int)H)}, lse.options());
   float* db = nullptr;
   if (dbias.has_value()) {
@@ -309,7 +319,7 @@ Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const 
   }
   check_hip(llmt::launch_attn_bwd(dout.data_ptr(), qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
                                   dqkv.data_ptr(), delta.data_ptr<float>(), dq.data_ptr<float>(), db, (int)B, (int)T,
-                                  (int)H, make_dropout(dropout_p, dropout_seed), cur_stream()),
+                                  (int)H, make_dropout(dropout_p, dropout_seed), cur_stream(), delta_in.has_value()),
             "attn_bwd");
   return dqkv;
 }
@@ -346,7 +356,7 @@ void wgrad_gemm(const Tensor& dy, const Tensor& x, Tensor c, int64_t split, int6
 // epilogue 0 -> (out, None); 1 -> (u, gelu(u)); 2 -> (du = acc * gelu'(u), None) with dbias += colsum.
 std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tensor& b, bool b_kn, int64_t epilogue,
                                                      const c10::optional<Tensor>& bias, const c10::optional<Tensor>& u,
-                                                     c10::optional<Tensor> dbias) {
+                                                     c10::optional<Tensor> dbias, int64_t seq_len) {
   check_gpu(a, "a");
   check_gpu(b, "b");
   check_dtype(a, at::kBFloat16, "a");
@@ -356,7 +366,7 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tens
   const int64_t N = b_kn ? b.size(1) : b.size(0);
   TORCH_CHECK((b_kn ? b.size(0) : b.size(1)) == K, "gemm_fused: inner dimensions differ");
   TORCH_CHECK(K % 64 == 0 && K >= 256 && N % 8 == 0, "gemm_fused: needs K % 64 == 0, K >= 256, N % 8 == 0");
-  TORCH_CHECK(epilogue >= 0 && epilogue <= 2, "gemm_fused: epilogue must be 0, 1 or 2");
+  TORCH_CHECK(epilogue >= 0 && epilogue <= 3, "gemm_fused: epilogue must be 0, 1, 2 or 3");
   // 16-byte LDS-DMA / vector stores on every operand, 4-byte DMA of the bias
   TORCH_CHECK((uintptr_t)a.data_ptr() % 16 == 0 && (uintptr_t)b.data_ptr() % 16 == 0,
               "gemm_fused: operands must be 16-byte aligned");
@@ -386,8 +396,14 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tens
     out2 = at::empty({M, N}, a.options());
     g.c2 = out2->data_ptr();
   }
-  if (epilogue == 2) {
-    TORCH_CHECK(u.has_value(), "gemm_fused: epilogue 2 needs u");
+  if (epilogue == 3) {
+    TORCH_CHECK(seq_len > 0 && M % seq_len == 0 && N % 64 == 0, "gemm_fused: epilogue 3 needs seq_len | M, 64 | N");
+    out2 = at::empty({M / seq_len, N / 64, seq_len}, a.options().dtype(at::kFloat));
+    g.delta = out2->data_ptr<float>();
+    g.T = (int)seq_len;
+  }
+  if (epilogue >= 2) {
+    TORCH_CHECK(u.has_value(), "gemm_fused: epilogue 2/3 needs u");
     check_gpu(*u, "u");
     check_dtype(*u, at::kBFloat16, "u");
     TORCH_CHECK(u->dim() == 2 && u->size(0) == M && u->size(1) == N, "gemm_fused: u must be [M, N]");
@@ -472,11 +488,11 @@ TORCH_LIBRARY(llmtrain_hip, m) {
         " int dropout_seed=0) -> ()");
   m.def("attn_fwd(Tensor qkv, int B, int T, int H, float dropout_p=0., int dropout_seed=0) -> (Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, int B, int T, int H, float dropout_p=0.,"
-        " int dropout_seed=0, Tensor(a!)? dbias=None) -> Tensor");
+        " int dropout_seed=0, Tensor(a!)? dbias=None, Tensor? delta=None) -> Tensor");
   m.def("dropout_mask(int n, float p, int seed, Tensor like) -> Tensor");
   m.def("wgrad_gemm(Tensor dy, Tensor x, Tensor(a!) c, int split=0, int tile=0) -> ()");
   m.def("gemm_fused(Tensor a, Tensor b, bool b_kn, int epilogue, Tensor? bias=None, Tensor? u=None,"
-        " Tensor(a!)? dbias=None) -> (Tensor, Tensor?)");
+        " Tensor(a!)? dbias=None, int seq_len=0) -> (Tensor, Tensor?)");
   m.def("sumsq(Tensor x) -> Tensor");
   m.def("adamw_flat(Tensor(a!) param, Tensor grad, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor(d!)? shadow,"
         " float lr, float beta1, float beta2, float eps, float weight_decay, int step, Tensor? grad_scale) -> ()");

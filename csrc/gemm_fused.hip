@@ -7,6 +7,10 @@
 //   0  C = bf16(acc + bias)                      (bias optional)
 //   1  U = bf16(acc + bias), C2 = bf16(gelu(U))  (fc forward: pre-activation kept for backward)
 //   2  C = bf16(acc * gelu'(U)), dbias += colsum(C)   (proj dX: GELU backward + fc bias grad)
+//   3  C = bf16(acc), delta[b, h, t] = sum_d C[m, 64h + d] * U[m, 64h + d], dbias += colsum(C)
+//      (attention out-proj dX = dO; U = the attention output O: the flash-attention backward's
+//      row constant and, without dropout, the V part of the qkv bias gradient — each wave's 64
+//      output columns are exactly one head, so the per-head dot product never leaves the wave)
 //
 // Why: in the GPT MLP (reference models/gpt.py:94-105, nn.Linear -> nn.GELU -> nn.Linear) the
 // library GEMM writes the pre-activation, a separate pass reads it and writes gelu(u), and in the
@@ -89,7 +93,7 @@ __device__ __forceinline__ float gelu_grad(float u) {
 // VMEM ops each epilogue issues unconditionally (a lower bound is what the counted waits need)
 template <int EPI>
 struct EpiOps {
-  static constexpr int value = EPI == 0 ? 16 : 32;
+  static constexpr int value = EPI == 0 ? 16 : (EPI == 3 ? 48 : 32);
 };
 
 // one 256-byte LDS-DMA op (4 bytes per lane), M0 saved/restored like dma16
@@ -186,8 +190,10 @@ struct Args {
   bf16_raw* C;
   bf16_raw* C2;          // EPI 1: gelu output
   const bf16_raw* bias;  // EPI 0/1 (optional for 0)
-  const bf16_raw* U;     // EPI 2: pre-activation
-  float* dbias;          // EPI 2: column sums (optional)
+  const bf16_raw* U;     // EPI 2: pre-activation; EPI 3: attention output O
+  float* dbias;          // EPI 2/3: column sums (optional)
+  float* delta;          // EPI 3: [M / T, N / 64, T] per-head row dot products
+  int T;                 // EPI 3: rows per sequence
   int lda, ldb, ldc, ldu;
   int M, N, K;
   int tiles_m, tiles_n, ntiles, nwg;
@@ -295,7 +301,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
   const __amdgpu_buffer_rsrc_t rc2 = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(EPI == 1 ? p.C2 : p.C), (short)0, p.M * p.ldc * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(EPI == 2 ? p.U : p.C), (short)0, p.M * (EPI == 2 ? p.ldu : p.ldc) * 2, 0x00020000);
+      (void*)(EPI >= 2 ? p.U : p.C), (short)0, p.M * (EPI >= 2 ? p.ldu : p.ldc) * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rdel = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(EPI == 3 ? p.delta : (float*)p.C), (short)0, EPI == 3 ? p.M * (p.N / 64) * 4 : 0, 0x00020000);
 
   // Software pipeline over the stage stream (2-slot ring of 64-deep stages; stage g+1 lands while
   // stage g computes).  Iteration g runs its four k16 MFMA groups with every fragment read issued
@@ -411,7 +419,43 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
         off[it] = (m < p.M && n < p.N) ? (m * p.ldc + n) * 2 : kOob;
       }
       asm volatile("" ::: "memory");
-      if (EPI == 2) {
+      if (EPI == 3) {
+        u32x4 oraw[2];
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          const int m = mw + 16 * mf + 8 * it + (lane >> 3);
+          const int uoff = (m < p.M && n < p.N) ? (m * p.ldu + n) * 2 : kOob;
+          oraw[it] = __builtin_amdgcn_raw_buffer_load_b128(ru, uoff, 0, 0);
+        }
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          __builtin_amdgcn_sched_barrier(0);
+          const ushort8_t ov = __builtin_bit_cast(ushort8_t, oraw[it]);
+          float o[8];
+          float dot = 0.f;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            o[k] = bf2f(f2bf(vals[it][k]));  // the bf16 dO the attention backward reads
+            dot = fmaf(o[k], bf2f(ov[k]), dot);
+            csum[k] += o[k];
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(o)), rc, off[it], 0, 0);
+          // the 8 lanes of one row segment (lane & 7) hold the head's 64 columns
+          dot += __shfl_xor(dot, 1, 64);
+          dot += __shfl_xor(dot, 2, 64);
+          dot += __shfl_xor(dot, 4, 64);
+          const int m = mw + 16 * mf + 8 * it + (lane >> 3);
+          int doff = kOob;
+          if (q == 0 && m < p.M && nw < p.N) {
+            const int bb = m / p.T, t = m - bb * p.T;
+            doff = ((bb * (p.N >> 6) + (nw >> 6)) * p.T + t) * 4;
+          }
+          // unconditional (dropped past the descriptor): the counted waits see a fixed op count
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dot), rdel, doff, 0, 0);
+          asm volatile("" : "+v"(csum[0]), "+v"(csum[1]), "+v"(csum[2]), "+v"(csum[3]), "+v"(csum[4]),
+                       "+v"(csum[5]), "+v"(csum[6]), "+v"(csum[7]));
+        }
+      } else if (EPI == 2) {
         u32x4 uraw[2];
 #pragma unroll
         for (int it = 0; it < 2; ++it) {
@@ -451,7 +495,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
         }
       }
     }
-    if (EPI == 2 && p.dbias != nullptr) {  // column sums over the wave's 128 rows: lanes sharing q
+    if (EPI >= 2 && p.dbias != nullptr) {  // column sums over the wave's 128 rows: lanes sharing q
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float v = csum[k];
@@ -479,9 +523,12 @@ hipError_t launch_gemm_fused(const GemmFusedArgs& g, hipStream_t stream) {
   using namespace fgemm;
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
   if (g.K < 4 * BK || g.K % BK || g.N % 8 || g.lda % 8 || g.ldb % 8 || g.ldc % 8) return hipErrorInvalidValue;
-  if (g.epilogue < 0 || g.epilogue > 2) return hipErrorInvalidValue;
+  if (g.epilogue < 0 || g.epilogue > 3) return hipErrorInvalidValue;
   if (g.epilogue == 1 && g.c2 == nullptr) return hipErrorInvalidValue;
-  if (g.epilogue == 2 && (g.u == nullptr || g.ldu % 8)) return hipErrorInvalidValue;
+  if (g.epilogue >= 2 && (g.u == nullptr || g.ldu % 8)) return hipErrorInvalidValue;
+  if (g.epilogue == 3 && (g.delta == nullptr || g.T <= 0 || g.M % g.T || g.N % 64 ||
+                          (long long)g.M * (g.N / 64) * 4 >= (1LL << 31) - 64))
+    return hipErrorInvalidValue;
   // 32-bit signed buffer offsets over every operand
   const long long lim = (1LL << 31) - 64;
   if ((long long)g.M * g.lda * 2 >= lim || (long long)g.M * g.ldc * 2 >= lim ||
@@ -495,6 +542,8 @@ hipError_t launch_gemm_fused(const GemmFusedArgs& g, hipStream_t stream) {
   a.bias = (const bf16_raw*)g.bias;
   a.U = (const bf16_raw*)g.u;
   a.dbias = g.dbias;
+  a.delta = g.delta;
+  a.T = g.T;
   a.lda = g.lda;
   a.ldb = g.ldb;
   a.ldc = g.ldc;
@@ -530,7 +579,9 @@ hipError_t launch_gemm_fused(const GemmFusedArgs& g, hipStream_t stream) {
     case 2: launch_one<false, 1>(a, stream); break;
     case 3: launch_one<true, 1>(a, stream); break;
     case 4: launch_one<false, 2>(a, stream); break;
-    default: launch_one<true, 2>(a, stream); break;
+    case 5: launch_one<true, 2>(a, stream); break;
+    case 6: launch_one<false, 3>(a, stream); break;
+    default: launch_one<true, 3>(a, stream); break;
   }
   return hipGetLastError();
 }

@@ -122,6 +122,8 @@ struct GemmFusedArgs {
   const void* u = nullptr;
   int ldu = 0;
   float* dbias = nullptr;
+  float* delta = nullptr;  // epilogue 3: per-head row dot products of C and U, [M / T, N / 64, T]
+  int T = 0;               // epilogue 3: rows per sequence
   int M = 0, N = 0, K = 0;
   int epilogue = 0;
 };
@@ -138,8 +140,10 @@ hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, int B, int T,
 // (the qkv projection's bias gradient); `delta` [B, H, T] f32 and `dq_part`
 // (attn_bwd_workspace_floats(B, T, H) floats) scratch
 long attn_bwd_workspace_floats(int B, int T, int H);
+// delta_ready: `delta` already holds rowsum(dO * O) (the out-proj dX GEMM's epilogue 3, which
+// then also added the V part of `dbias`): the delta pass is skipped
 hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse,
                            void* dqkv, float* delta, float* dq_part, float* dbias, int B, int T,
-                           int H, DropoutArgs dropout, hipStream_t stream);
+                           int H, DropoutArgs dropout, hipStream_t stream, bool delta_ready = false);
 
 }  // namespace llmt

@@ -441,12 +441,24 @@ class FusedGPTEngine:
             # attention output projection
             self._wgrad(self._g(blk.attn.out_proj.weight), dy_lp, a.att)
             wo = self._w(blk.attn.out_proj.weight)
-            datt = ops.linear_dx(dy_lp, wo) if self.fused_gemm_bwd else torch.mm(dy_lp, wo)
+            attn_drop = st.site(2 + 3 * i)
+            qkv_bg = self._g(blk.attn.qkv_proj.bias)
+            delta = None
+            if self.fused_gemm_bwd:
+                # dO plus the attention backward's row constants (and, without attention dropout,
+                # the V part of the qkv-bias gradient) from one GEMM epilogue
+                # (not taken -> delta None: attn_bwd computes it and the V-bias part itself)
+                d = qkv_bg.numel() // 3
+                datt, delta = ops.linear_dx_attn(
+                    dy_lp, wo, a.att, seqlen, v_bias_grad=qkv_bg[2 * d :] if attn_drop[0] == 0 else None
+                )
+            else:
+                datt = torch.mm(dy_lp, wo)
             del dy_lp
             # the qkv-bias gradient (column sums of dqkv) is fused into the attention backward
             dqkv = ops.attn_bwd(
-                datt, a.qkv, a.att, a.lse, bsz, seqlen, self.n_heads, dropout=st.site(2 + 3 * i),
-                qkv_bias_grad=self._g(blk.attn.qkv_proj.bias),
+                datt, a.qkv, a.att, a.lse, bsz, seqlen, self.n_heads, dropout=attn_drop,
+                qkv_bias_grad=qkv_bg, delta=delta,
             )
             del datt
             self._wgrad(self._g(blk.attn.qkv_proj.weight), dqkv, a.h1)

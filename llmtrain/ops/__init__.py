@@ -127,12 +127,16 @@ def attn_fwd(qkv, bsz: int, seqlen: int, n_heads: int, dropout=(0.0, 0)):
     return ref.attn_fwd(qkv, bsz, seqlen, n_heads, p, seed)
 
 
-def attn_bwd(dout, qkv, out, lse, bsz: int, seqlen: int, n_heads: int, dropout=(0.0, 0), qkv_bias_grad=None):
+def attn_bwd(
+    dout, qkv, out, lse, bsz: int, seqlen: int, n_heads: int, dropout=(0.0, 0), qkv_bias_grad=None, delta=None
+):
     """Attention backward -> packed ``dqkv``; ``qkv_bias_grad`` (fp32 ``[3d]``), when given,
-    accumulates ``colsum(dqkv)`` (fused into the kernels on GPU)."""
+    accumulates ``colsum(dqkv)`` (fused into the kernels on GPU).  ``delta`` (GPU): the row
+    constants ``rowsum(dO * O)`` already computed by :func:`linear_dx_attn`, which then also added
+    the V part of ``qkv_bias_grad`` when there is no dropout; the delta pass is skipped."""
     p, seed = dropout
     if _on_gpu(dout):
-        return hip_ops().attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads, p, seed, qkv_bias_grad)
+        return hip_ops().attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads, p, seed, qkv_bias_grad, delta)
     dqkv = ref.attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads, p, seed)
     if qkv_bias_grad is not None:
         ref.colsum_accum(dqkv, qkv_bias_grad)
@@ -151,6 +155,10 @@ FGEMM_MAX_A_BYTES = int(os.environ.get("LLMTRAIN_FGEMM_MAX_A_MB", "64")) * 2**20
 # (same-box, micro-batch 128: +0.9 %, 994.9k/995.5k vs 985.8k/986.8k tok/s); adding the plain dX
 # GEMMs (-0.4 %) or the forward GEMMs (-1.6 %) at this size loses (scripts/abn.sh).
 FGEMM_ANY_SIZE = frozenset(filter(None, os.environ.get("LLMTRAIN_FGEMM_ANY_SIZE", "dx_gelu").split(",")))
+
+
+# LLMTRAIN_ATTN_DX_FUSED=0 keeps the attention out-projection dX on the plain paths (A/B knob)
+ATTN_DX_FUSED = os.environ.get("LLMTRAIN_ATTN_DX_FUSED", "1") != "0"
 
 
 def _fgemm_ok(a: torch.Tensor, k: int, n: int, *others: torch.Tensor | None, op: str = "") -> bool:
@@ -195,6 +203,26 @@ def linear_dx_gelu_bwd(dy, w, u, dbias=None):
     if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy, dy.shape[1], w.shape[1], w, u, op="dx_gelu"):
         return hip_ops().gemm_fused(dy, w, True, 2, None, u, dbias)[0]
     return gelu_bwd(torch.mm(dy, w), u, dbias)
+
+
+def linear_dx_attn(dy, w, att, seqlen: int, v_bias_grad=None):
+    """Data gradient of the attention output projection, ``dO = dy @ w``, plus the flash-attention
+    backward's row constants ``delta[b, h, t] = sum_d dO * O`` (``att`` = the attention output O)
+    and, when given, ``v_bias_grad += colsum(dO)`` (the V part of the qkv bias gradient, valid
+    without attention dropout).  GPU: one fused GEMM epilogue (csrc/gemm_fused.hip, epilogue 3)
+    replacing the separate pass that re-read dO and O.  Returns ``(dO, delta)``; ``delta`` is None
+    when the GEMM is not taken (the attention backward then computes it itself, and the caller
+    must leave ``v_bias_grad`` to it)."""
+    if (
+        ATTN_DX_FUSED
+        and _on_gpu(dy)
+        and dy.dtype == torch.bfloat16
+        and dy.shape[0] % seqlen == 0
+        and w.shape[1] % 64 == 0
+        and _fgemm_ok(dy, dy.shape[1], w.shape[1], w, att, op="dx_attn")
+    ):
+        return tuple(hip_ops().gemm_fused(dy, w, True, 3, None, att, v_bias_grad, seqlen))
+    return torch.mm(dy, w), None
 
 
 def wgrad_accum(dst, dy, x) -> None:

@@ -275,3 +275,21 @@ def test_gemm_fused_dgelu(gpu_device, M, N, K, b_kn):
     _close(du, du_ref, 2e-2, 1e-2, "du")
     # the bias gradient sums exactly the bf16 values written
     _close(dbias, 0.5 + du.float().sum(0), 1e-3, 1e-4, "dbias")
+
+
+@pytest.mark.parametrize("M,N,K,T", [(4096, 768, 768, 1024), (1536, 768, 768, 512), (600, 256, 256, 300), (2048, 1600, 1600, 256)])
+@pytest.mark.parametrize("b_kn", [True, False])
+def test_gemm_fused_attn_dx_delta(gpu_device, M, N, K, T, b_kn):
+    """Epilogue 3: dO = dY @ W plus the attention backward's delta = per-head rowsum(dO * O) and
+    the V-bias colsum(dO); delta must equal what the attention backward's own pass computes."""
+    a, w, b, _ = _gemm_operands(M, N, K, b_kn, gpu_device, 7 * M + N)
+    g = torch.Generator(device="cpu").manual_seed(13)
+    o = torch.randn(M, N, generator=g).to(gpu_device, torch.bfloat16)
+    dbias = torch.full((N,), 0.25, device=gpu_device)
+    do, delta = hip().gemm_fused(a, b, b_kn, 3, None, o, dbias, T)
+    _close(do, a.float() @ w.float().t(), 2e-2, 1e-2, "dO")
+    H = N // 64
+    ref_delta = (do.float() * o.float()).view(M // T, T, H, 64).sum(-1).permute(0, 2, 1)
+    assert delta.shape == (M // T, H, T)
+    _close(delta, ref_delta, 1e-3, 1e-3, "delta")
+    _close(dbias, 0.25 + do.float().sum(0), 1e-3, 1e-4, "dbias_v")

@@ -162,6 +162,10 @@ def ln(M: int = 65536, d: int = 768) -> None:
     ms = timeit(lambda: ops.layernorm_bwd(dy, xs, mu, rs, w, dres, dw, db, None, True, dp))
     gb = M * d * (2 + 4 + 4 + 4 + 2) / 1e9
     print(json.dumps({"op": "ln_bwd", "ms": round(ms, 4), "GB/s": round(gb / ms * 1e3, 1)}), flush=True)
+    u = torch.randn(M, 4 * d, device=dev, dtype=torch.bfloat16)
+    ms = timeit(lambda: ops.gelu_fwd(u))
+    gb = M * 4 * d * 4 / 1e9
+    print(json.dumps({"op": "gelu_fwd", "ms": round(ms, 4), "GB/s": round(gb / ms * 1e3, 1)}), flush=True)
 
 
 def attn(B: int = 32, T: int = 1024, H: int = 12) -> list[dict]:

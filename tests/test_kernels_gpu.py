@@ -81,9 +81,9 @@ def test_cross_entropy_fwd_bwd(gpu_device, M, V, Vp):
     assert torch.all(lg[:, V:] == 0)
 
 
-def test_gelu_fwd_bwd(gpu_device):
+@pytest.mark.parametrize("M,F", [(2048, 3072), (40000, 3072), (1001, 200)])
+def test_gelu_fwd_bwd(gpu_device, M, F):
     g = torch.Generator(device="cpu").manual_seed(3)
-    M, F = 2048, 3072
     u = (2 * torch.randn(M, F, generator=g)).to(gpu_device, torch.bfloat16)
     _close(hip().gelu_fwd(u), ref.gelu_fwd(u.float()), 1e-2, 1e-2, "gelu")
     dg = torch.randn(M, F, generator=g).to(gpu_device, torch.bfloat16)
@@ -92,7 +92,9 @@ def test_gelu_fwd_bwd(gpu_device):
     du = hip().gelu_bwd(dg, u, dbias)
     du_r = ref.gelu_bwd(dg.float(), u.float(), dbias_r)
     _close(du, du_r, 2e-2, 2e-2, "du")
-    _close(dbias, dbias_r, 0.3, 1e-2, "dbias")
+    _close(dbias, dbias_r, 0.3 * (M / 2048) ** 0.5, 1e-2, "dbias")  # rounding noise grows ~sqrt(M)
+    # and exactly (up to fp32 summation order) the column sums of the bf16 du the kernel wrote
+    _close(dbias, du.float().sum(0), 1e-2, 1e-4, "dbias vs colsum(du)")
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])

@@ -190,6 +190,20 @@ Tensor gelu_fwd(const Tensor& u) {
   return g;
 }
 
+Tensor scale(const Tensor& x, const Tensor& s) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.is_contiguous() && x.numel() % 8 == 0, "scale: contiguous x with numel % 8 == 0");
+  TORCH_CHECK(s.is_cuda() && s.numel() == 1, "scale: s must be a 1-element GPU tensor");
+  check_dtype(s, at::kFloat, "s");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor y = at::empty_like(x);
+  if (x.numel() > 0)
+    check_hip(llmt::launch_scale(x.data_ptr(), y.data_ptr(), s.data_ptr<float>(), is_lowp(x, "x"), x.numel(),
+                                 cur_stream()),
+              "scale");
+  return y;
+}
+
 Tensor gelu_bwd(const Tensor& dg, const Tensor& u, const c10::optional<Tensor>& dbias) {
   check_gpu(dg, "dg");
   check_gpu(u, "u");
@@ -481,6 +495,7 @@ TORCH_LIBRARY(llmtrain_hip, m) {
         " float dropout_p=0., int dropout_seed=0) -> (Tensor, Tensor)");
   m.def("cross_entropy_fwd_bwd(Tensor(a!) logits, Tensor labels, int vocab, Tensor row_weight) -> Tensor");
   m.def("gelu_fwd(Tensor u) -> Tensor");
+  m.def("scale(Tensor x, Tensor s) -> Tensor");
   m.def("gelu_bwd(Tensor dg, Tensor u, Tensor(a!)? dbias) -> Tensor");
   m.def("colsum_accum(Tensor dy, Tensor(a!) out) -> ()");
   m.def("embedding_fwd(Tensor ids, Tensor wte, Tensor wpe, float dropout_p=0., int dropout_seed=0) -> Tensor");
@@ -503,6 +518,7 @@ TORCH_LIBRARY_IMPL(llmtrain_hip, CUDA, m) {
   m.impl("layernorm_bwd", &layernorm_bwd);
   m.impl("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd);
   m.impl("gelu_fwd", &gelu_fwd);
+  m.impl("scale", &scale);
   m.impl("gelu_bwd", &gelu_bwd);
   m.impl("colsum_accum", &colsum_accum);
   m.impl("embedding_fwd", &embedding_fwd);

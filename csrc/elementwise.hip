@@ -73,6 +73,21 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const void* __restrict__ 
   }
 }
 
+// y = x * (*scale) with the scale read from device memory (an autograd upstream gradient: no
+// host sync), fp32 math, one rounding: replaces x.float() * s -> .to(bf16) (three passes).
+template <bool BF16>
+__global__ __launch_bounds__(256) void scale_kernel(const void* __restrict__ x, void* __restrict__ y,
+                                                    const float* __restrict__ scale, long n8) {
+  const float s = *scale;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float f[8];
+    ld8<BF16>(x, i, f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] *= s;
+    st8<BF16>(y, i, f);
+  }
+}
+
 // Column-tiled [M, F] pass: a workgroup owns 64 column-vectors (512 columns) and a strip of rows;
 // its 4 waves split the strip, keep 8 f32 column partials per lane, reduce through LDS and add
 // one f32 atomic per column.  OP 0 = gelu backward (+ optional dbias), OP 1 = column sum only.
@@ -222,6 +237,15 @@ hipError_t launch_gelu_fwd(const void* u, void* g, bool bf16, long long n, hipSt
   const int grid = stride_grid(n8, 256, 256 * 16);
   if (bf16) hipLaunchKernelGGL(gelu_fwd_kernel<true>, dim3(grid), dim3(256), 0, stream, u, g, n8);
   else hipLaunchKernelGGL(gelu_fwd_kernel<false>, dim3(grid), dim3(256), 0, stream, u, g, n8);
+  return hipGetLastError();
+}
+
+hipError_t launch_scale(const void* x, void* y, const float* scale, bool bf16, long long n, hipStream_t stream) {
+  if (n % 8 != 0) return hipErrorInvalidValue;
+  const long n8 = n / 8;
+  const int grid = stride_grid(n8, 256, 256 * 16);
+  if (bf16) hipLaunchKernelGGL(scale_kernel<true>, dim3(grid), dim3(256), 0, stream, x, y, scale, n8);
+  else hipLaunchKernelGGL(scale_kernel<false>, dim3(grid), dim3(256), 0, stream, x, y, scale, n8);
   return hipGetLastError();
 }
 

@@ -64,6 +64,8 @@ hipError_t launch_cross_entropy_fwd_bwd(void* logits, bool bf16, const int64_t* 
                                         int V, hipStream_t stream);
 
 // ---- elementwise / reductions -----------------------------------------------------------
+// y = x * scale[0] (device scalar), fp32 math, bf16 or fp32 storage; n % 8 == 0
+hipError_t launch_scale(const void* x, void* y, const float* scale, bool bf16, long long n, hipStream_t stream);
 hipError_t launch_gelu_fwd(const void* u, void* g, bool bf16, long long n, hipStream_t stream);
 // du = dg * gelu'(u); dbias (optional, [F]) += colsum(du); tensors are [M, F]
 hipError_t launch_gelu_bwd(const void* dg, const void* u, void* du, float* dbias, bool bf16,

@@ -32,6 +32,7 @@ __all__ = [
     "linear_dx_gelu_bwd",
     "linear_fwd",
     "linear_fwd_gelu",
+    "scale",
     "sumsq",
 ]
 
@@ -84,6 +85,14 @@ def cross_entropy_fwd_bwd(logits, labels, vocab: int, row_weight):
     if _on_gpu(logits):
         return hip_ops().cross_entropy_fwd_bwd(logits, labels, vocab, row_weight)
     return ref.cross_entropy_fwd_bwd(logits, labels, vocab, row_weight)
+
+
+def scale(x, s):
+    """``x * s`` for a 0-/1-element fp32 device scalar ``s`` (an autograd upstream gradient):
+    one HIP pass with fp32 math and a single rounding on GPU, no host sync."""
+    if _on_gpu(x) and x.is_contiguous() and x.numel() % 8 == 0 and x.dtype in (torch.bfloat16, torch.float32):
+        return hip_ops().scale(x, s.reshape(1).float())
+    return (x.float() * s.float()).to(x.dtype)
 
 
 def gelu_fwd(u):

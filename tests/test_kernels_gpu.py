@@ -295,3 +295,16 @@ def test_gemm_fused_attn_dx_delta(gpu_device, M, N, K, T, b_kn):
     assert delta.shape == (M // T, H, T)
     _close(delta, ref_delta, 1e-3, 1e-3, "delta")
     _close(dbias, 0.25 + do.float().sum(0), 1e-3, 1e-4, "dbias_v")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_scale_device_scalar(gpu_device, dtype):
+    """``scale``: x * s with s read from device memory, fp32 math and one rounding — matches the
+    fp32 product rounded once (the LM-head weight-gradient operand ``go * hf``)."""
+    g = torch.Generator(device="cpu").manual_seed(7)
+    x = torch.randn(1001, 768, generator=g).to(gpu_device, dtype)
+    s = torch.tensor(1.0 / 3.0, device=gpu_device)
+    y = hip().scale(x, s.reshape(1))
+    want = (x.float() * s).to(dtype)
+    assert y.dtype == dtype and y.shape == x.shape
+    assert torch.equal(y, want)

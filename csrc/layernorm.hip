@@ -10,6 +10,9 @@
 // gradient of the projection whose output was added into this residual stream) with per-lane
 // register partials over a grid-stride run of rows, a cross-wave LDS reduction, then one fp32
 // atomic per column per workgroup.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -280,8 +283,8 @@ void launch_fwd_c(const LnFwdArgs& a, hipStream_t st) {
 template <int MAXC>
 void launch_bwd_c(const LnBwdArgs& a, hipStream_t st) {
   const size_t shm = (size_t)kBwdWaves * a.d * sizeof(float);
-  // exactly one resident wave of workgroups (a second partial wave would be a pure tail: every
-  // workgroup runs the same number of rows)
+  // a whole number of resident waves of workgroups (a partial extra wave would be a pure tail:
+  // every workgroup runs the same number of rows)
   static int resident[2][2] = {{0, 0}, {0, 0}};
   int& per_cu = resident[a.dy_bf16 ? 1 : 0][a.dx_lp != nullptr ? 1 : 0];
   if (per_cu == 0) {
@@ -294,7 +297,14 @@ void launch_bwd_c(const LnBwdArgs& a, hipStream_t st) {
     else
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, a.dx_lp ? ln_bwd_kernel<MAXC, float, true>
                                                               : ln_bwd_kernel<MAXC, float, false>, 256, shm);
-    per_cu = (n > 0 ? n : 4) * (cus > 0 ? cus : 256);
+    // LLMT_LN_BWD_WAVES: resident waves of workgroups per launch (A/B knob; default 4 for rows of <= 768
+    // columns, 1 above: GPT-2 XL d = 1600 measured 80.0k (1) vs 79.7k (4) tok/s).  More
+    // than one lets the hardware dispatcher balance rows onto CUs the side stream's weight-
+    // gradient GEMMs free up, at the cost of more column-partial atomics (124M / micro-batch 128
+    // same-box: 1 -> 1.0224M, 2 -> 1.0259M, 4 -> 1.0276M, 8 -> 1.0243M tok/s).
+    const char* e = std::getenv("LLMT_LN_BWD_WAVES");
+    const int waves = e ? std::max(1, std::atoi(e)) : (MAXC <= 3 ? 4 : 1);
+    per_cu = (n > 0 ? n : 4) * (cus > 0 ? cus : 256) * waves;
   }
   const int grid = stride_grid((long long)(a.M + kBwdWaves - 1) / kBwdWaves, 1, per_cu);
 #define LN_BWD(TDY, LP)                                                                         \

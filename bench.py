@@ -1,9 +1,14 @@
 #!/usr/bin/env python3
 """Headline benchmark: GPT-2 124M training throughput on MI355X (BASELINE.json metric).
 
-    python bench.py --gpus N --steps K --warmup W            # N=1 directly
+    python bench.py --gpus N --steps K --warmup W            # spawns N ranks itself when N > 1
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
-        --master-port P bench.py --gpus N --steps K --warmup W   # N>1, one rank per GPU (RCCL)
+        --master-port P bench.py --gpus N --steps K --warmup W   # or under an external launcher
+
+With ``--gpus N > 1`` and no ``WORLD_SIZE`` in the environment, this process starts
+``torch.distributed.run --nproc-per-node N`` as a CHILD process (before touching the GPU) and
+exits with its code, so ``python bench.py --gpus 8`` really measures 8 RCCL ranks.  Every rank
+asserts ``dist.get_world_size() == N`` and the ``nccl`` (= RCCL) backend.
 
 Each rank runs the real ``llmtrain`` Trainer (fused GPT engine, hand-written gfx950 kernels,
 bucketed RCCL all-reduce, fused AdamW) on the reference GPT-2 124M architecture (V=50257,
@@ -11,7 +16,10 @@ T=1024, d=768, 12 layers, 12 heads, d_ff=3072, tied embeddings, random init) in 
 synthetic token windows of the full block size.  W untimed warm-up steps, then EXACTLY K timed
 optimizer steps (forward + backward + gradient all-reduce + clip + AdamW + LR schedule — nothing
 skipped) bracketed by barrier + synchronize; the slowest rank's time counts.  Weak scaling: the
-per-GPU batch is fixed, so the aggregate tokens/s is reported for the whole job.
+per-GPU batch is fixed, so the aggregate tokens/s is reported for the whole job, plus per-rank
+tokens/s and the exposed all-reduce time (communication not hidden behind the backward).
+
+``--device cpu`` (gloo, fp32, ``--model tiny``) exists for the CPU contract tests only.
 """
 
 from __future__ import annotations
@@ -19,6 +27,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,7 +42,29 @@ BASELINE_METRIC = "tokens/sec/GPU GPT-2-124M DDP at 1/2/4/8 MI355X; val-loss par
 MODELS = {
     "gpt2-124m": dict(vocab_size=50257, block_size=1024, d_model=768, n_layers=12, n_heads=12, d_ff=3072),
     "gpt2-xl": dict(vocab_size=50257, block_size=1024, d_model=1600, n_layers=48, n_heads=25, d_ff=6400),
+    "tiny": dict(vocab_size=512, block_size=64, d_model=64, n_layers=2, n_heads=2, d_ff=128),  # CPU tests
 }
+MODEL_LABEL = {"gpt2-124m": "GPT-2 124M", "gpt2-xl": "GPT-2 XL 1.5B", "tiny": "tiny (CPU contract test)"}
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """Run this script under ``torch.distributed.run`` with ``n`` local ranks (child process,
+    never ``exec``: nothing here has touched the GPU yet) and return its exit code."""
+    cmd = [
+        sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv,
+    ]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this driver
+    env.setdefault("OMP_NUM_THREADS", "4")
+    print(f"bench: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
 
 
 def make_config(args: argparse.Namespace, world: int):
@@ -41,9 +73,13 @@ def make_config(args: argparse.Namespace, world: int):
     model = dict(MODELS[args.model], name="gpt", dropout=args.dropout, tie_embeddings=True)
     if args.path == "module":
         model["extra"] = {"fused": False}
+    gpu = args.device == "cuda"
+    if not gpu:
+        model.setdefault("extra", {})["fused"] = args.path == "fused"
     payload = {
         "schema_version": 1,
-        "run": {"name": f"bench-{args.model}", "seed": 1337, "device": "cuda", "precision": "bf16"},
+        "run": {"name": f"bench-{args.model}", "seed": 1337, "device": args.device,
+                "precision": "bf16" if gpu else "fp32"},
         "model": model,
         "data": {
             "name": "synthetic_tokens",
@@ -59,9 +95,9 @@ def make_config(args: argparse.Namespace, world: int):
             "weight_decay": 0.1,
             "warmup_steps": 0,
             "max_grad_norm": 1.0,
-            "extra": {"bucket_cap_mb": args.bucket_mb},
+            "extra": {"bucket_cap_mb": args.bucket_mb, "grad_reduce_dtype": args.grad_reduce_dtype},
         },
-        "ddp": {"enabled": world > 1, "backend": "nccl"},
+        "ddp": {"enabled": world > 1, "backend": "nccl" if gpu else "gloo"},
         "mlflow": {"enabled": False},
         "logging": {"log_to_file": False},
         "output": {"root_dir": "/tmp/llmtrain_bench_runs"},
@@ -78,13 +114,23 @@ def main() -> int:
     ap.add_argument("--micro-batch", type=int, default=128, help="sequences per GPU per micro-step")
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--grad-reduce-dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="dtype of the gradient all-reduce payload (fused path)")
     ap.add_argument("--path", choices=["fused", "module"], default="fused")
     ap.add_argument("--dropout", type=float, default=0.0, help="model dropout (reference default 0.1)")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda", help="cpu: contract tests only")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])
+    world = int(world_env or "1")
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+        print(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        return 2
+    gpu = args.device == "cuda"
     from llmtrain.parallel.dist import setup_ddp, teardown_ddp
     from llmtrain.training.trainer import Trainer
 
@@ -92,20 +138,30 @@ def main() -> int:
     ddp_state = None
     if world > 1:
         ddp_state = setup_ddp(cfg)
-    else:
+        got_world, backend = dist.get_world_size(), dist.get_backend()
+        want_backend = "nccl" if gpu else "gloo"
+        if got_world != args.gpus or backend != want_backend:
+            raise RuntimeError(f"rank {ddp_state.rank}: world={got_world} backend={backend}, "
+                               f"expected world={args.gpus} backend={want_backend}")
+    elif gpu:
         torch.cuda.set_device(0)
     trainer = Trainer(cfg, ddp_state=ddp_state)
     batches = trainer.batch_stream()
     rank = ddp_state.rank if ddp_state else 0
+    dev = torch.device("cuda", torch.cuda.current_device()) if gpu else torch.device("cpu")
+    drain = getattr(trainer.model, "drain_exposed_comm_ms", None)
 
     def barrier() -> None:
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        if gpu:
+            torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         loss, _ = trainer.train_step(batches)
     barrier()
+    if drain is not None:
+        drain()
     t0 = time.perf_counter()
     tokens = 0
     for _ in range(args.steps):
@@ -114,17 +170,21 @@ def main() -> int:
     barrier()
     elapsed = time.perf_counter() - t0
     final_loss = float(loss.item())
+    comm = drain() if drain is not None else []
+    comm_ms = sum(comm) / len(comm) if comm else 0.0
     want = args.steps * cfg.trainer.micro_batch_size * cfg.trainer.grad_accum_steps * cfg.model.block_size
     if tokens != want:  # a short data shard would silently shrink the per-GPU batch
         raise RuntimeError(f"rank {rank}: timed {tokens} tokens, expected {want}")
 
-    elapsed_t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    tokens_t = torch.tensor([tokens], dtype=torch.float64, device="cuda")
+    mine = torch.tensor([elapsed, float(tokens), comm_ms], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(elapsed_t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tokens_t, op=dist.ReduceOp.SUM)
-    elapsed = float(elapsed_t.item())
-    total_tokens = float(tokens_t.item())
+        gathered = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(gathered, mine)
+    else:
+        gathered = [mine]
+    rows = [g.tolist() for g in gathered]
+    elapsed = max(r[0] for r in rows)
+    total_tokens = sum(r[1] for r in rows)
     tps = total_tokens / elapsed
     if rank == 0:
         from llmtrain.utils.flops import mfu, training_flops_per_token
@@ -143,10 +203,10 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if gpu else "fp32",
             "data": "synthetic (seeded Markov token windows, full block_size), random-init weights",
             "config": {
-                "model": "GPT-2 124M" if args.model == "gpt2-124m" else "GPT-2 XL 1.5B",
+                "model": MODEL_LABEL[args.model],
                 "global_batch": global_batch,
                 "seq_len": cfg.model.block_size,
                 "parallelism": f"dp{world}",
@@ -154,17 +214,24 @@ def main() -> int:
                 "grad_accum": cfg.trainer.grad_accum_steps,
                 "path": args.path,
                 "dropout": args.dropout,
+                "grad_reduce_dtype": args.grad_reduce_dtype,
+                "backend": dist.get_backend() if world > 1 else None,
             },
             "tokens_per_sec_per_gpu": round(tps / world, 1),
-            "mfu": round(mfu(tps / world, per_tok), 4),
+            "per_rank_tokens_per_sec": [round(r[1] / r[0], 1) for r in rows],
+            "exposed_allreduce_ms": [round(r[2], 3) for r in rows],
             "final_loss": round(final_loss, 4),
-            "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 2),
-            "alloc_retries": int(torch.cuda.memory_stats().get("num_alloc_retries", 0)),
-            "device_mallocs": int(torch.cuda.memory_stats().get("num_device_alloc", 0)),
-            "reserved_gib": round(torch.cuda.memory_reserved() / 2**30, 2),
-            "tuned_gemm_table": bool(getattr(trainer, "tuned_gemms", False)),
-            "device_free_total_gib": [round(v / 2**30, 1) for v in torch.cuda.mem_get_info()],
         }
+        if gpu:
+            result.update({
+                "mfu": round(mfu(tps / world, per_tok), 4),
+                "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 2),
+                "alloc_retries": int(torch.cuda.memory_stats().get("num_alloc_retries", 0)),
+                "device_mallocs": int(torch.cuda.memory_stats().get("num_device_alloc", 0)),
+                "reserved_gib": round(torch.cuda.memory_reserved() / 2**30, 2),
+                "tuned_gemm_table": bool(getattr(trainer, "tuned_gemms", False)),
+                "device_free_total_gib": [round(v / 2**30, 1) for v in torch.cuda.mem_get_info()],
+            })
         print(json.dumps(result), flush=True)
     if ddp_state is not None:
         teardown_ddp()

@@ -22,6 +22,8 @@ from __future__ import annotations
 
 import contextlib
 import logging
+import time
+from collections import deque
 from collections.abc import Iterator
 from dataclasses import dataclass
 from typing import Any
@@ -97,6 +99,8 @@ class FlatDataParallel(nn.Module):
         self._works: list[tuple[Bucket, Any, torch.Tensor | None]] = []
         self._sync = True
         self._armed = False
+        self._exposed: tuple[Any, Any] | float | None = None
+        self._exposed_hist: deque[tuple[Any, Any] | float] = deque(maxlen=256)
         engine.grad_ready = self._on_segment_ready
         if broadcast_parameters and self.world_size > 1:
             with torch.no_grad():
@@ -159,11 +163,21 @@ class FlatDataParallel(nn.Module):
         self._works.append((bucket, work, staged))
 
     def finish_gradient_sync(self) -> None:
-        """Wait (stream-side on RCCL) for every launched bucket and finalise averaging."""
+        """Wait (stream-side on RCCL) for every launched bucket and finalise averaging.
+
+        The wait is bracketed by timing events on the compute stream: their distance is the
+        *exposed* communication time — how long the optimizer waited for all-reduces still in
+        flight after the backward's last kernel (:meth:`exposed_comm_ms`)."""
         if not self._armed:
             return
         if any(r != 0 for r in self._remaining):
             raise RuntimeError(f"gradient buckets never completed: {self._remaining}")
+        on_gpu = self._store.grad.is_cuda
+        if on_gpu:
+            t_start = torch.cuda.Event(enable_timing=True)
+            t_start.record()
+        else:
+            t_host = time.perf_counter()
         for bucket, work, staged in self._works:
             work.wait()
             view = self._store.grad[bucket.start : bucket.start + bucket.numel]
@@ -171,5 +185,31 @@ class FlatDataParallel(nn.Module):
                 view.copy_(staged)
             if not self._avg_native:
                 view.div_(self.world_size)
+        if on_gpu:
+            t_end = torch.cuda.Event(enable_timing=True)
+            t_end.record()
+            self._exposed = (t_start, t_end)
+        else:
+            self._exposed = 1000.0 * (time.perf_counter() - t_host)
+        self._exposed_hist.append(self._exposed)
         self._works.clear()
         self._armed = False
+
+    def exposed_comm_ms(self) -> float | None:
+        """Exposed all-reduce time of the last synchronised step in ms (``None`` before the first).
+        Reading it synchronises on that step's end event — call it at log intervals only."""
+        return None if self._exposed is None else self._resolve(self._exposed)
+
+    def drain_exposed_comm_ms(self) -> list[float]:
+        """Exposed all-reduce ms of every step synchronised since the last drain (oldest first,
+        at most 256); clears the history.  Synchronises on the newest step's end event."""
+        out = [self._resolve(ex) for ex in self._exposed_hist]
+        self._exposed_hist.clear()
+        return out
+
+    @staticmethod
+    def _resolve(ex: tuple[Any, Any] | float) -> float:
+        if isinstance(ex, float):
+            return ex
+        ex[1].synchronize()
+        return float(ex[0].elapsed_time(ex[1]))

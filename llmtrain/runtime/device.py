@@ -17,7 +17,7 @@ import torch
 
 from llmtrain.config.schemas import RunConfig
 
-__all__ = ["RuntimePolicy", "resolve_policy", "seed_everything"]
+__all__ = ["RuntimePolicy", "decorrelate_rank_streams", "resolve_policy", "seed_everything"]
 
 
 @dataclass(frozen=True)
@@ -64,3 +64,20 @@ def seed_everything(seed: int) -> None:
     torch.manual_seed(seed)
     if torch.cuda.is_available():
         torch.cuda.manual_seed_all(seed)
+
+
+def decorrelate_rank_streams(rank: int) -> int:
+    """Give each data-parallel rank its own torch RNG stream from here on.
+
+    Called AFTER the model is built (parameter init stays identical on every rank) and again after
+    a resume restored rank 0's checkpointed RNG state onto every rank.  Every rank draws the same
+    value from the (identical) generator state and reseeds with that value mixed with its rank, so
+    dropout masks — the fused engine's per-forward site seed and the module path's ``nn.Dropout``
+    on CPU or GPU — differ across ranks like the reference's unseeded per-process generators, yet a
+    run stays reproducible.  Returns the new seed."""
+    draw = int(torch.randint(0, 2**62, (1,)).item())
+    seed = (draw ^ ((rank + 1) * 0x9E3779B97F4A7C15)) % (2**63 - 1)
+    torch.manual_seed(seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed_all(seed)
+    return seed

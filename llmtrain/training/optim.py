@@ -4,8 +4,8 @@ Reference: ``torch.optim.AdamW(model.parameters(), lr, weight_decay)`` with defa
 decay applied to every parameter (``training/trainer.py:93-97``), and
 ``clip_grad_norm_`` before each step (``trainer.py:390-393``).
 
-:class:`FusedAdamW` keeps exactly the ``torch.optim.AdamW`` ``state_dict`` layout (per-parameter
-``step`` fp32 scalar, ``exp_avg``, ``exp_avg_sq``; same ``param_groups`` keys) so checkpoints
+:class:`FusedAdamW` keeps exactly the ``torch.optim.AdamW`` ``state_dict`` layout (a distinct
+per-parameter ``step`` fp32 scalar, ``exp_avg``, ``exp_avg_sq``; same ``param_groups`` keys) so checkpoints
 move between this build and the reference in both directions, but the update itself is ONE
 HIP kernel over the flat buffers: it reads the fp32 master weight, gradient and both moments,
 applies the (device-side) gradient-clipping coefficient, writes the new master weight, both
@@ -77,6 +77,22 @@ class FusedAdamW(torch.optim.Optimizer):
                 st["step"] = self._step_tensor
                 st["exp_avg"] = m
                 st["exp_avg_sq"] = v
+
+    def state_dict(self) -> dict[str, Any]:
+        """torch.optim.AdamW layout with a DISTINCT fp32 ``step`` tensor per parameter.
+
+        Internally every parameter shares one step counter (the update is one kernel over the
+        flat buffers).  Exporting that shared tensor would survive ``torch.save`` as an alias, and
+        ``torch.optim.AdamW`` (non-capturable) increments ``state["step"]`` in place once per
+        parameter — a shared counter would then advance by #params per step and corrupt the bias
+        correction after a resume on the module path or in the reference trainer
+        (reference ``training/checkpoint.py:53-68``, ``trainer.py:93-97``)."""
+        sd = super().state_dict()
+        sd["state"] = {
+            k: {**st, "step": st["step"].detach().clone()} if "step" in st else dict(st)
+            for k, st in sd["state"].items()
+        }
+        return sd
 
     def load_state_dict(self, state_dict: dict[str, Any]) -> None:
         super().load_state_dict(state_dict)

@@ -18,7 +18,9 @@ What changes on the MI355X path:
   reference disables replay under DDP);
 * ``peak_memory`` reports ``torch.cuda.max_memory_allocated`` (GiB) on GPU;
 * optional ``trainer.extra``: ``keep_last_k``, ``fail_at_step`` (fault injection),
-  ``profile`` (torch.profiler window), ``bucket_cap_mb``, ``grad_reduce_dtype``.
+  ``profile`` (torch.profiler window), ``bucket_cap_mb``, ``grad_reduce_dtype``;
+* ``train/allreduce_ms`` (max over ranks) logs the exposed gradient all-reduce time of the flat
+  reducer — the part of the communication NOT hidden behind the backward.
 """
 
 from __future__ import annotations
@@ -43,7 +45,7 @@ from llmtrain.parallel.dist import DDPState
 from llmtrain.registry import initialize_registries
 from llmtrain.registry.data import get_data_module
 from llmtrain.registry.models import get_model_adapter
-from llmtrain.runtime.device import resolve_policy, seed_everything
+from llmtrain.runtime.device import decorrelate_rank_streams, resolve_policy, seed_everything
 from llmtrain.runtime.tuning import enable_tuned_gemms
 from llmtrain.tracking import NullTracker, Tracker
 from llmtrain.training.checkpoint import CheckpointManager, CheckpointPayload, restore_rng_states
@@ -160,6 +162,7 @@ class Trainer:
         if self._is_ddp_active:
             self._model = wrap_data_parallel(model, cfg, self._device)
             verify_replicas(model.parameters(), device=self._metric_device(), tag="after data-parallel wrap")
+            decorrelate_rank_streams(self._rank)  # per-rank dropout masks; init stayed identical
 
         self._optimizer = build_optimizer(unwrap(self._model), cfg.trainer.lr, cfg.trainer.weight_decay)
         self._scheduler = self._build_scheduler(self._optimizer)
@@ -251,6 +254,8 @@ class Trainer:
         self._optimizer.load_state_dict(payload["optimizer_state_dict"])
         self._scheduler.load_state_dict(payload["scheduler_state_dict"])
         restore_rng_states(payload["rng_states"])
+        if self._is_ddp_active:  # the checkpoint holds rank 0's streams: split them again
+            decorrelate_rank_streams(self._rank)
         store = getattr(self._raw_model, "flat_store", None)
         if store is not None:
             store.sync_shadow(force=True)
@@ -456,11 +461,14 @@ class Trainer:
                     raise FloatingPointError(f"non-finite training loss {avg_loss} at step {step}")
                 extra_metrics = self._device_metrics(tps)
                 if self._is_ddp_active:
+                    comm_ms = self._exposed_comm_ms()
                     per_rank = self._gather_scalars(
                         avg_loss=avg_loss, lr=lr, tokens_per_sec=tps, step_time=step_time,
-                        tokens_total=float(tokens_local_total),
+                        tokens_total=float(tokens_local_total), allreduce_ms=comm_ms,
                     )
+                    worst_comm_ms = comm_ms
                     if per_rank is not None:
+                        worst_comm_ms = max(v["allreduce_ms"] for v in per_rank)
                         for r, vals in enumerate(per_rank):
                             self._tracker.log_metrics(
                                 {
@@ -469,6 +477,7 @@ class Trainer:
                                     f"train/tokens_per_sec_rank_{r}": vals["tokens_per_sec"],
                                     f"train/step_time_sec_rank_{r}": vals["step_time"],
                                     f"train/tokens_total_rank_{r}": vals["tokens_total"],
+                                    f"train/allreduce_ms_rank_{r}": vals["allreduce_ms"],
                                 },
                                 step=step,
                             )
@@ -485,6 +494,7 @@ class Trainer:
                                 "train/tokens_per_sec": global_tps,
                                 "train/tokens_total": float(tokens_global_total),
                                 "train/step_time_sec": step_time,
+                                "train/allreduce_ms": worst_comm_ms,
                                 **self._device_metrics(global_tps / self._world_size),
                             },
                             step=step,
@@ -552,6 +562,13 @@ class Trainer:
             parameter_count=n_params,
             trainable_parameter_count=n_trainable,
         )
+
+    def _exposed_comm_ms(self) -> float:
+        """Exposed gradient all-reduce time of the last step (ms): the flat reducer's wait after
+        the backward's last kernel.  torch DDP (module path) does not expose it: 0.0 there."""
+        probe = getattr(self._model, "exposed_comm_ms", None)
+        value = probe() if probe is not None else None
+        return float(value) if value is not None else 0.0
 
     def _device_metrics(self, tokens_per_sec_per_gpu: float) -> dict[str, float]:
         """GPU-only extras: model FLOPs utilisation (vs dense bf16 peak) and peak memory."""

@@ -7,6 +7,9 @@ from __future__ import annotations
 import argparse
 import importlib.util
 import json
+import os
+import subprocess
+import sys
 from pathlib import Path
 
 import pytest
@@ -33,7 +36,8 @@ def test_metric_matches_baseline_json() -> None:
 def test_every_rank_gets_full_micro_batches(world: int, mb: int, accum: int) -> None:
     bench = _bench()
     args = argparse.Namespace(model="gpt2-124m", micro_batch=mb, grad_accum=accum, dropout=0.0,
-                              path="fused", warmup=1, steps=2, bucket_mb=64.0)
+                              path="fused", warmup=1, steps=2, bucket_mb=64.0, device="cuda",
+                              grad_reduce_dtype="fp32")
     cfg = bench.make_config(args, world)
     n = cfg.data.extra["train_sequences"]
     assert n // world >= mb * accum
@@ -47,3 +51,47 @@ def test_every_rank_gets_full_micro_batches(world: int, mb: int, accum: int) -> 
     dm.setup(small, tokenizer=None)
     batch = next(iter(dm.train_dataloader()))
     assert batch["input_ids"].shape == (mb, 8)
+
+
+def _run_bench(*argv: str, env_extra: dict[str, str] | None = None) -> subprocess.CompletedProcess:
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(PYTHONPATH=str(ROOT), OMP_NUM_THREADS="2", **(env_extra or {}))
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--device", "cpu", "--model", "tiny", "--steps", "2",
+           "--warmup", "1", "--micro-batch", "2", *argv]
+    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+
+
+def _json_line(stdout: str) -> dict:
+    lines = [ln for ln in stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, stdout  # rank 0 prints exactly one line
+    return json.loads(lines[0])
+
+
+@pytest.mark.slow
+def test_bench_gpus_2_spawns_two_ranks() -> None:
+    """``bench.py --gpus 2`` without a launcher starts 2 ranks itself (gloo on CPU here, RCCL on the
+    GPU box) — the number it prints is a real 2-rank job, not one GPU with a warning."""
+    proc = _run_bench("--gpus", "2")
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    res = _json_line(proc.stdout)
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2"
+    assert res["config"]["backend"] == "gloo"
+    assert len(res["per_rank_tokens_per_sec"]) == 2 and len(res["exposed_allreduce_ms"]) == 2
+    assert res["config"]["global_batch"] == 2 * 2
+    assert res["value"] > 0 and res["steps"] == 2 and res["warmup"] == 1
+
+
+def test_bench_rejects_world_size_mismatch() -> None:
+    proc = _run_bench("--gpus", "2", env_extra={"WORLD_SIZE": "1"})
+    assert proc.returncode == 2
+    assert "WORLD_SIZE=1" in proc.stderr
+
+
+def test_bench_single_rank_cpu_contract() -> None:
+    proc = _run_bench("--gpus", "1")
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    res = _json_line(proc.stdout)
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert key in res
+    assert res["n_gpus"] == 1 and res["higher_is_better"] is True and res["scaling"] == "weak"

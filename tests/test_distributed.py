@@ -207,6 +207,35 @@ def test_trainer_ddp_metrics_and_rank0_io(tmp_path: Path, fused: bool) -> None:
     assert r0["val"] == pytest.approx(r1["val"])  # global val loss is the same on all ranks
 
 
+def _dropout_stream_worker(rank: int, world: int, port: int, out_dir: str) -> None:
+    _init(rank, world, port)
+    from llmtrain.training.trainer import Trainer
+
+    model = {"name": "gpt", "vocab_size": 32, "block_size": 8, "d_model": 64, "n_layers": 1, "n_heads": 2,
+             "d_ff": 64, "dropout": 0.5, "extra": {"fused": True}}
+    cfg = RunConfig.model_validate(minimal_payload(
+        model=model, ddp={"enabled": True}, run={"name": "t", "seed": 11},
+        trainer={"max_steps": 2, "warmup_steps": 0, "micro_batch_size": 2, "grad_accum_steps": 1},
+    ))
+    state = DDPState(rank=rank, world_size=world, local_rank=rank, is_main=rank == 0)
+    tr = Trainer(cfg, ddp_state=state)
+    params = torch.cat([p.detach().reshape(-1) for p in tr.model.parameters()])
+    # the fused engine's per-forward dropout site seed and a module-path nn.Dropout mask
+    site_seed = int(torch.randint(0, 2**31 - 1, (1,)).item())
+    mask = torch.nn.functional.dropout(torch.ones(256), 0.5, training=True)
+    torch.save({"params": params, "site_seed": site_seed, "mask": mask}, Path(out_dir) / f"drop{rank}.pt")
+    dist.destroy_process_group()
+
+
+def test_dropout_streams_differ_per_rank_but_init_is_shared(tmp_path: Path) -> None:
+    mp.spawn(_dropout_stream_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "drop0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "drop1.pt", weights_only=True)
+    assert torch.equal(r0["params"], r1["params"])
+    assert r0["site_seed"] != r1["site_seed"]
+    assert not torch.equal(r0["mask"], r1["mask"])
+
+
 @pytest.mark.slow
 def test_torchrun_cli_end_to_end(tmp_path: Path) -> None:
     cfg = yaml_safe_load(REPO / "configs" / "presets" / "ddp_smoke.yaml")

@@ -12,7 +12,7 @@ import torch
 from llmtrain.inference import GraphDecoder, generate
 from llmtrain.models.gpt import GPT
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("gpu_device")]
 
 
 def _model() -> GPT:

@@ -21,6 +21,10 @@
 
 int main(int argc, char** argv) {
   const int B = argc > 1 ? std::atoi(argv[1]) : 32, T = 1024, H = 12, D = 64;
+  llmt::AttnDims dims;
+  dims.B = B;
+  dims.T = T;
+  dims.H = H;
   const size_t nqkv = (size_t)B * T * 3 * H * D, nout = (size_t)B * T * H * D, nrow = (size_t)B * H * T;
   std::vector<unsigned short> h(nqkv);
   unsigned s = 12345;
@@ -40,11 +44,11 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
-  for (int i = 0; i < 5; ++i) CHECK(llmt::launch_attn_fwd(qkv, out, lse, B, T, H, llmt::DropoutArgs{}, 0));
+  for (int i = 0; i < 5; ++i) CHECK(llmt::launch_attn_fwd(qkv, out, lse, dims, llmt::DropoutArgs{}, 0));
   std::vector<float> ms;
   for (int i = 0; i < 30; ++i) {
     CHECK(hipEventRecord(a, 0));
-    CHECK(llmt::launch_attn_fwd(qkv, out, lse, B, T, H, llmt::DropoutArgs{}, 0));
+    CHECK(llmt::launch_attn_fwd(qkv, out, lse, dims, llmt::DropoutArgs{}, 0));
     CHECK(hipEventRecord(b, 0));
     CHECK(hipEventSynchronize(b));
     float t;

@@ -1,4 +1,4 @@
-// Causal flash-attention backward, head_dim 64, for gfx950 (MI355X).
+// Causal flash-attention backward, head_dim <= 64, for gfx950 (MI355X).
 //
 // Replaces the autograd backward of reference models/gpt.py:56-69 (softmax + two batched
 // matmuls over materialised [B, H, T, T] tensors).  P is recomputed from Q, K and the forward's
@@ -22,7 +22,10 @@
 //    the <= T/256 planes per row straight into the packed bf16 dqkv;
 //  * branch-free buffer loads (rows past T read as zero), double-buffered Q/dO and dS images,
 //    one barrier per query tile; heaviest key blocks dispatched first, the key blocks of one
-//    (batch, head) on one XCD (shared Q/dO in its L2).
+//    (batch, head) on one XCD (shared Q/dO in its L2);
+//  * SMALLHD (head dims < 64, multiples of 8) zero-fills the missing dims at load time; KMASK
+//    (key padding) zeroes P of this lane's key when it is padded — one per-lane flag, because the
+//    key sits on the MFMA lane here (rows the forward marked dead have lse = +inf, so P = 0).
 
 #include "attention_common.h"
 
@@ -44,7 +47,7 @@ constexpr int kDeltaRows = 256;
 __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restrict__ dout,
                                                          const bf16_raw* __restrict__ out,
                                                          float* __restrict__ delta, float* __restrict__ dbias_v,
-                                                         int T, int H) {
+                                                         int T, int H, int hd) {
   __shared__ float red[4][kHD];
   const int bh = blockIdx.y;
   const int b = bh / H, h = bh - b * H;
@@ -56,10 +59,10 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
     const int t = blockIdx.x * kDeltaRows + 32 * it + rl;
     dv[it] = ushort8_t{0, 0, 0, 0, 0, 0, 0, 0};
     ov[it] = dv[it];
-    if (t < T) {
+    if (t < T && 8 * sub < hd) {
       const long row = ((long)b * T + t) * H + h;
-      dv[it] = *reinterpret_cast<const ushort8_t*>(dout + row * kHD + 8 * sub);
-      ov[it] = *reinterpret_cast<const ushort8_t*>(out + row * kHD + 8 * sub);
+      dv[it] = *reinterpret_cast<const ushort8_t*>(dout + row * hd + 8 * sub);
+      ov[it] = *reinterpret_cast<const ushort8_t*>(out + row * hd + 8 * sub);
     }
   }
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -94,9 +97,9 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
     for (int i = 0; i < 8; ++i) red[wv][8 * sub + i] = csum[i];
   }
   __syncthreads();
-  if (threadIdx.x < kHD) {
+  if (threadIdx.x < hd) {
     const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    atomicAdd(dbias_v + h * kHD + threadIdx.x, s);
+    atomicAdd(dbias_v + h * hd + threadIdx.x, s);
   }
 }
 
@@ -108,7 +111,8 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
 // gradient (column sums of dQ) leaves the workgroup as 64 atomics per kDqRows rows.
 constexpr int kDqRows = 64;
 __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const float* __restrict__ part, bf16_raw* __restrict__ dqkv,
-                                                             float* __restrict__ dbias, int T, int H, int nkb, long plane) {
+                                                             float* __restrict__ dbias, int T, int H, int hd, int nkb,
+                                                             long plane) {
   __shared__ float red[4][kHD];
   const int bh = blockIdx.x;
   const int b = bh / H, h = bh - b * H;
@@ -141,8 +145,8 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const float* __rest
 #pragma unroll
   for (int it = 0; it < kSweeps; ++it) {
     const int t = t0 + 32 * it;
-    if (t < T) {
-      *reinterpret_cast<ushort8_t*>(dqkv + (((long)b * T + t) * 3L * H + h) * kHD + 8 * c) = pack8(f[it]);
+    if (t < T && 8 * c < hd) {  // the partial planes are 64 wide; dims >= hd are zero
+      *reinterpret_cast<ushort8_t*>(dqkv + ((long)b * T + t) * 3L * H * hd + (long)h * hd + 8 * c) = pack8(f[it]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) csum[j] += f[it][j];
     }
@@ -160,9 +164,9 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const float* __rest
     for (int j = 0; j < 8; ++j) red[wv][8 * c + j] = csum[j];
   }
   __syncthreads();
-  if (threadIdx.x < kHD) {
+  if (threadIdx.x < hd) {
     const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    atomicAdd(dbias + h * kHD + threadIdx.x, s);
+    atomicAdd(dbias + h * hd + threadIdx.x, s);
   }
 }
 
@@ -180,14 +184,15 @@ __device__ __forceinline__ float buf_load_f32(__amdgpu_buffer_rsrc_t r, int byte
 // 16 rows a ds_read_b128 lane group touches land on 16 distinct chunks (all 64 banks)
 __device__ __forceinline__ int kt_off(int d, int key) { return d * kKvBlk + ((((key >> 3) ^ (d & 15))) << 3) + (key & 7); }
 
-template <bool DROPOUT>
+template <bool DROPOUT, bool KMASK, bool SMALLHD>
 __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __restrict__ qkv,
                                                           const bf16_raw* __restrict__ dout,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta,
                                                           bf16_raw* __restrict__ dqkv,
                                                           float* __restrict__ dq_part, float* __restrict__ dbias,
-                                                          int T, int H, int nkb, DropoutArgs dr) {
+                                                          int T, int H, int nkb, DropoutArgs dr, int hd_arg,
+                                                          float scale_arg, const uint8_t* __restrict__ key_valid) {
   __shared__ __attribute__((aligned(16))) bf16_raw kt_lds[kHD * kKvBlk];             // K^T, 32 KB
   __shared__ __attribute__((aligned(16))) bf16_raw qd_lds[2][2][kQTile * kHD];      // [buf][Q|dO] 32 KB
   __shared__ __attribute__((aligned(16))) bf16_raw ds_lds[2][kKvBlk * kQTile];      // [buf][key][q] 64 KB
@@ -200,17 +205,23 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   const int bh = blockIdx.x;                 // all key blocks of one (b, h) share an XCD
   const int kb = (int)blockIdx.y;            // ... and the heaviest key blocks (most query tiles) go first
   const int b = bh / H, h = bh - b * H;
-  const long row_stride = 3L * H * kHD;
-  const bf16_raw* base = qkv + (long)b * T * row_stride + (long)h * kHD;
-  const bf16_raw* dobase = dout + (long)b * T * H * kHD + (long)h * kHD;  // [B, T, H, 64]
-  const long out_stride = (long)H * kHD;
+  const int hd = SMALLHD ? hd_arg : kHD;  // head dim in memory; tiles and fragments stay 64 wide
+  const long row_stride = 3L * H * hd;
+  const bf16_raw* base = qkv + (long)b * T * row_stride + (long)h * hd;
+  const bf16_raw* dobase = dout + (long)b * T * H * hd + (long)h * hd;  // [B, T, H, hd]
+  const long out_stride = (long)H * hd;
   const float* lse_bh = lse + ((long)b * H + h) * T;
   const float* delta_bh = delta + ((long)b * H + h) * T;
   // descriptors bounded at row T of this (b, h): rows past the sequence load as zeros
   const __amdgpu_buffer_rsrc_t r_q = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0,
-                                                                        (int)((T - 1) * row_stride + kHD) * 2, 0x00020000);
+                                                                        (int)((T - 1) * row_stride + hd) * 2, 0x00020000);
+  // K/V of the block's keys: bounded past row T - 1's V section (a descriptor ending at row T - 1's
+  // Q section would read the last key's K and V as zeros)
+  const __amdgpu_buffer_rsrc_t r_kv = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0,
+                                                                         (int)((T - 1) * row_stride + 3 * hd * H) * 2,
+                                                                         0x00020000);
   const __amdgpu_buffer_rsrc_t r_do = __builtin_amdgcn_make_buffer_rsrc((void*)dobase, (short)0,
-                                                                         (int)((T - 1) * out_stride + kHD) * 2, 0x00020000);
+                                                                         (int)((T - 1) * out_stride + hd) * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t r_lse = __builtin_amdgcn_make_buffer_rsrc((void*)lse_bh, (short)0, T * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t r_del = __builtin_amdgcn_make_buffer_rsrc((void*)delta_bh, (short)0, T * 4, 0x00020000);
 
@@ -219,16 +230,22 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   const int kw0 = kblk0 + 32 * wave;  // first key of this wave
   const int key = kw0 + col;          // this lane's key
 
-  constexpr float scale = 0.125f;
-  constexpr float c = scale * 1.4426950408889634f;
+  const float scale = SMALLHD ? scale_arg : 0.125f;
+  const float c = scale * 1.4426950408889634f;
+  // key padding: this lane's key (on the MFMA lane) is excluded from P when padded
+  const bool kvalid = !KMASK || (key < T && key_valid[(long)b * T + key] != 0);
 
   // K and V fragments of this lane's key: B operands of S = Q K^T and dP = dO V^T
   bf16x8 kf[4], vf[4];
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
     const int off = (int)(key * row_stride + 16 * kk + 8 * half) * 2;
-    kf[kk] = __builtin_bit_cast(bf16x8, buf_load16(r_q, off + kHD * H * 2));
-    vf[kk] = __builtin_bit_cast(bf16x8, buf_load16(r_q, off + 2 * kHD * H * 2));
+    kf[kk] = __builtin_bit_cast(bf16x8, buf_load16(r_kv, off + hd * H * 2));
+    vf[kk] = __builtin_bit_cast(bf16x8, buf_load16(r_kv, off + 2 * hd * H * 2));
+    if (SMALLHD && 16 * kk + 8 * half >= hd) {
+      kf[kk] = __builtin_bit_cast(bf16x8, ushort8_t{0, 0, 0, 0, 0, 0, 0, 0});
+      vf[kk] = kf[kk];
+    }
   }
   // K^T image for dQ = dS K (B operand read 8 keys at a time); written from the K fragments
 #pragma unroll
@@ -249,6 +266,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
       const int qrow = q0 + r;
       stg[i] = i == 0 ? buf_load16(r_q, (int)(qrow * row_stride + ch * 8) * 2)
                       : buf_load16(r_do, (int)(qrow * out_stride + ch * 8) * 2);
+      if (SMALLHD && ch * 8 >= hd) stg[i] = ushort8_t{0, 0, 0, 0, 0, 0, 0, 0};
     }
     if (threadIdx.x < 2 * kQTile) {
       const int qq = q0 + (threadIdx.x & (kQTile - 1));
@@ -305,6 +323,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
             if (DROPOUT) ddv[4 * rr + i] = dd[i];
             else dp[4 * rr + i] -= dd[i];
           }
+        }
+        if (KMASK && !kvalid) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) p[r] = 0.f;
         }
         if (!full && ((kw0 + 31 > qb0) || (kw0 + 32 > T) || (qb0 + 32 > T))) {
           // causal / sequence-end mask: element r is query qb0 + 4*half + (r&3) + 8(r>>2),
@@ -416,7 +438,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
 
   // ---- dK = scale * dK^T, dV = dV^T  -> dqkv[b, key, 1|2, h, :] ------------------------------
   if (key < T) {
-    bf16_raw* dst = dqkv + ((long)b * T + key) * row_stride + (long)h * kHD;
+    bf16_raw* dst = dqkv + ((long)b * T + key) * row_stride + (long)h * hd;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) {
 #pragma unroll
@@ -428,8 +450,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
           vv[i] = f2bf(dv[dt][4 * g + i]);
         }
         const int d = dt * 32 + 8 * g + 4 * half;
-        *reinterpret_cast<ushort4_t*>(dst + kHD * H + d) = kv;
-        *reinterpret_cast<ushort4_t*>(dst + 2 * kHD * H + d) = vv;
+        if (!SMALLHD || d < hd) {
+          *reinterpret_cast<ushort4_t*>(dst + hd * H + d) = kv;
+          *reinterpret_cast<ushort4_t*>(dst + 2 * hd * H + d) = vv;
+        }
       }
     }
   }
@@ -449,11 +473,11 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
     }
   }
   __syncthreads();
-  if (threadIdx.x < kHD) {
+  if (threadIdx.x < hd) {
     float acc = 0.f;
 #pragma unroll
     for (int w = 0; w < kBwdWaves; ++w) acc += bias_red[w][threadIdx.x];
-    atomicAdd(dbias + (2 * H + h) * kHD + threadIdx.x, acc);
+    atomicAdd(dbias + (2 * H + h) * hd + threadIdx.x, acc);
   }
 }
 
@@ -464,27 +488,43 @@ long attn_bwd_workspace_floats(int B, int T, int H) {
   return nkb * B * H * (long)T * attn::kHD;
 }
 
+template <bool DROPOUT, bool KMASK, bool SMALLHD>
+static void launch_bwd_variant(dim3 grid, hipStream_t stream, const bf16_raw* qkv, const bf16_raw* dout,
+                               const float* lse, const float* delta, bf16_raw* dqkv, float* dq_part, float* dbias,
+                               const AttnDims& d, int nkb, DropoutArgs dr) {
+  hipLaunchKernelGGL((attn::attn_bwd_kernel<DROPOUT, KMASK, SMALLHD>), grid, dim3(512), 0, stream, qkv, dout, lse,
+                     delta, dqkv, dq_part, dbias, d.T, d.H, nkb, dr, d.hd, d.scale, d.key_valid);
+}
+
 hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse, void* dqkv,
-                           float* delta, float* dq_part, float* dbias, int B, int T, int H,
-                           DropoutArgs dropout, hipStream_t stream, bool delta_ready) {
-  if (B <= 0 || T <= 0 || H <= 0 || T > 65535) return hipErrorInvalidValue;
+                           float* delta, float* dq_part, float* dbias, const AttnDims& d, DropoutArgs dropout,
+                           hipStream_t stream, bool delta_ready) {
+  const int B = d.B, T = d.T, H = d.H, hd = d.hd;
+  if (B <= 0 || T <= 0 || H <= 0 || T > 65535 || hd <= 0 || hd > attn::kHD || hd % 8 != 0) return hipErrorInvalidValue;
   const long rows = (long)B * T * H;
   if (!delta_ready)
     hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((T + attn::kDeltaRows - 1) / attn::kDeltaRows, B * H), dim3(256), 0, stream,
-                     (const bf16_raw*)dout, (const bf16_raw*)out, delta,
-                     dropout.thr == 0 && dbias != nullptr ? dbias + 2L * H * attn::kHD : nullptr, T, H);
+                       (const bf16_raw*)dout, (const bf16_raw*)out, delta,
+                       dropout.thr == 0 && dbias != nullptr ? dbias + 2L * H * hd : nullptr, T, H, hd);
   const int nkb = (T + attn::kKvBlk - 1) / attn::kKvBlk;
-  if (dropout.thr != 0)
-    hipLaunchKernelGGL(attn::attn_bwd_kernel<true>, dim3(B * H, nkb), dim3(512), 0, stream, (const bf16_raw*)qkv,
-                       (const bf16_raw*)dout, lse, delta, (bf16_raw*)dqkv, dq_part, dbias, T, H, nkb,
-                       dropout);
-  else
-    hipLaunchKernelGGL(attn::attn_bwd_kernel<false>, dim3(B * H, nkb), dim3(512), 0, stream, (const bf16_raw*)qkv,
-                       (const bf16_raw*)dout, lse, delta, (bf16_raw*)dqkv, dq_part, dbias, T, H, nkb,
-                       dropout);
+  const dim3 grid(B * H, nkb);
+  const bool drop = dropout.thr != 0, km = d.key_valid != nullptr, small = hd != attn::kHD;
+  const int variant = (drop ? 4 : 0) | (km ? 2 : 0) | (small ? 1 : 0);
+  auto q = (const bf16_raw*)qkv;
+  auto g = (const bf16_raw*)dout;
+  auto dq = (bf16_raw*)dqkv;
+  switch (variant) {
+    case 0: launch_bwd_variant<false, false, false>(grid, stream, q, g, lse, delta, dq, dq_part, dbias, d, nkb, dropout); break;
+    case 1: launch_bwd_variant<false, false, true>(grid, stream, q, g, lse, delta, dq, dq_part, dbias, d, nkb, dropout); break;
+    case 2: launch_bwd_variant<false, true, false>(grid, stream, q, g, lse, delta, dq, dq_part, dbias, d, nkb, dropout); break;
+    case 3: launch_bwd_variant<false, true, true>(grid, stream, q, g, lse, delta, dq, dq_part, dbias, d, nkb, dropout); break;
+    case 4: launch_bwd_variant<true, false, false>(grid, stream, q, g, lse, delta, dq, dq_part, dbias, d, nkb, dropout); break;
+    case 5: launch_bwd_variant<true, false, true>(grid, stream, q, g, lse, delta, dq, dq_part, dbias, d, nkb, dropout); break;
+    case 6: launch_bwd_variant<true, true, false>(grid, stream, q, g, lse, delta, dq, dq_part, dbias, d, nkb, dropout); break;
+    default: launch_bwd_variant<true, true, true>(grid, stream, q, g, lse, delta, dq, dq_part, dbias, d, nkb, dropout); break;
+  }
   hipLaunchKernelGGL(attn::attn_dq_reduce_kernel, dim3(B * H, (T + attn::kDqRows - 1) / attn::kDqRows), dim3(256), 0,
-                     stream, dq_part,
-                     (bf16_raw*)dqkv, dbias, T, H, nkb, rows * (long)attn::kHD);
+                     stream, dq_part, dq, dbias, T, H, hd, nkb, rows * (long)attn::kHD);
   return hipGetLastError();
 }
 

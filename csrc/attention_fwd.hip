@@ -1,4 +1,4 @@
-// Causal flash-attention forward, head_dim 64, bf16 in / bf16 out, for gfx950 (MI355X).
+// Causal flash-attention forward, head_dim <= 64, bf16 in / bf16 out, for gfx950 (MI355X).
 //
 // Replaces reference models/gpt.py:49-71 (qkv split, Q K^T / sqrt(hd), causal masked_fill,
 // softmax, P V), which materialises [B, H, T, T] fp32 scores; here nothing of size T^2 ever
@@ -20,7 +20,14 @@
 //  * one XOR swizzle of the 16-byte chunks of each 128-byte LDS row makes both the row reads
 //    (ds_read_b128, K as the A operand) and the transposed reads (V) bank-conflict free;
 //  * softmax in the exp2 domain (v_exp_f32), scale folded into one multiply;
-//  * heaviest (last) query blocks are dispatched first to shorten the causal tail.
+//  * heaviest (last) query blocks are dispatched first to shorten the causal tail;
+//  * SMALLHD: head dims below 64 (multiples of 8: the reference presets' 32 and 48) run the same
+//    64-wide tiles with the missing dims zero-filled at load time and never stored;
+//  * KMASK: key-padding mask (reference gpt.py:60-64) from one 64-bit word per 64-key tile (a
+//    scalar load: the tile's keys are wave-uniform); padded keys score -inf like future keys.  A
+//    row whose keys so far are ALL masked keeps m = -inf: its exponent offset is taken as 0 then
+//    (P = exp2(-inf) = 0, no inf - inf), and the first real key rescales with alpha = 0; rows that
+//    never saw a real key are written as O = 0, lse = +inf.
 #include "attention_common.h"
 
 namespace llmt {
@@ -30,11 +37,12 @@ constexpr int kFwdWaves = 4;
 constexpr int kQBlk = 32 * kFwdWaves;  // 128 query rows per workgroup
 constexpr int kKBlk = 64;              // keys per LDS tile
 
-template <bool DROPOUT>
+template <bool DROPOUT, bool KMASK, bool SMALLHD>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __restrict__ qkv,
                                                           bf16_raw* __restrict__ out,
                                                           float* __restrict__ lse, int T, int H,
-                                                          int nqb, DropoutArgs dr) {
+                                                          int nqb, DropoutArgs dr, int hd_arg, float c_arg,
+                                                          const uint64_t* __restrict__ key_bits) {
   __shared__ __attribute__((aligned(16))) bf16_raw smem[2][2][kKBlk * kHD];  // [buf][K|V][tile]
   const int lane = threadIdx.x & 63;
   // readfirstlane makes the wave index (and every tile/mask decision derived from it) provably
@@ -44,8 +52,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
   const int qb = nqb - 1 - (int)blockIdx.x;  // heavy blocks first
   const int bh = blockIdx.y;
   const int b = bh / H, h = bh - b * H;
-  const long row_stride = 3L * H * kHD;  // elements between consecutive tokens in qkv
-  const bf16_raw* base = qkv + (long)b * T * row_stride + (long)h * kHD;
+  const int hd = SMALLHD ? hd_arg : kHD;  // head dim in memory; tiles stay 64 wide
+  const long row_stride = 3L * H * hd;   // elements between consecutive tokens in qkv
+  const bf16_raw* base = qkv + (long)b * T * row_stride + (long)h * hd;
   // attention-probability dropout: plane seed per (b, h), element index q*T + key
   const uint32_t pseed = DROPOUT ? mix32(dr.seed + (uint32_t)bh * 0x9E3779B9u) : 0u;
 
@@ -58,7 +67,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
     ushort8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (q < T) v = *reinterpret_cast<const ushort8_t*>(base + (long)q * row_stride + 16 * kk + 8 * half);
+    if (q < T && (!SMALLHD || 16 * kk + 8 * half < hd))
+      v = *reinterpret_cast<const ushort8_t*>(base + (long)q * row_stride + 16 * kk + 8 * half);
     qf[kk] = __builtin_bit_cast(bf16x8, v);
   }
 
@@ -69,17 +79,21 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
   // iterations of compute to land instead of one.  Buffer loads bounded at row T of this (b, h):
   // keys past the sequence read as zeros without branches.
   const __amdgpu_buffer_rsrc_t rkv = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)base, (short)0, (int)(((long)T - 1) * row_stride + 3 * kHD * H) * 2, 0x00020000);
+      (void*)base, (short)0, (int)(((long)T - 1) * row_stride + 3 * hd * H) * 2, 0x00020000);
   ushort8_t st0[4], st1[4];
   auto load_tile = [&](ushort8_t(&st)[4], int tile) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c = threadIdx.x + 256 * i;
       const int r = c >> 3, ch = c & 7;
-      const int off = (int)(((long)(tile * kKBlk + r) * row_stride + ch * 8 + kHD * H) * 2);
+      const int off = (int)(((long)(tile * kKBlk + r) * row_stride + ch * 8 + hd * H) * 2);
       typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
       st[i] = __builtin_bit_cast(ushort8_t, __builtin_amdgcn_raw_buffer_load_b128(rkv, off, 0, 0));
-      st[2 + i] = __builtin_bit_cast(ushort8_t, __builtin_amdgcn_raw_buffer_load_b128(rkv, off + kHD * H * 2, 0, 0));
+      st[2 + i] = __builtin_bit_cast(ushort8_t, __builtin_amdgcn_raw_buffer_load_b128(rkv, off + hd * H * 2, 0, 0));
+      if (SMALLHD && ch * 8 >= hd) {  // the next head's columns: zero-fill the missing dims
+        st[i] = ushort8_t{0, 0, 0, 0, 0, 0, 0, 0};
+        st[2 + i] = st[i];
+      }
     }
   };
   auto store_tile = [&](const ushort8_t(&st)[4], int buf) {
@@ -97,7 +111,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
   o[0] = 0.f;
   o[1] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
-  constexpr float c = 0.125f * 1.4426950408889634f;  // (1/sqrt(64)) * log2(e)
+  const float c = SMALLHD ? c_arg : 0.125f * 1.4426950408889634f;  // softmax scale * log2(e)
+  const int nkw = (T + kKBlk - 1) / kKBlk;  // key-mask words per sequence
 
   load_tile(st0, 0);
   store_tile(st0, 0);
@@ -122,6 +137,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
         for (int kk = 0; kk < 4; ++kk) {
           const bf16x8 a = lds_row_read(Kt, kt * 32 + col, 2 * kk + half);
           s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[kk], s[kt], 0, 0, 0);
+        }
+      }
+      if (KMASK) {  // key padding: one word for the tile's 64 keys (wave-uniform scalar load)
+        const uint64_t mw = key_bits[(long)b * nkw + it];
+        if (mw != ~0ull) {
+          const uint64_t ml = mw >> (4 * half);  // register r of this lane half is key bit (r&3)+8(r>>2)+32kt
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              s[kt][r] = ((ml >> ((r & 3) + 8 * (r >> 2) + 32 * kt)) & 1ull) ? s[kt][r] : -INFINITY;
         }
       }
       // causal / sequence-end mask (diagonal tiles only) and the tile max, on RAW scores: the
@@ -149,13 +175,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
       // tile always rescales (m_run = -inf), and tile 0 gives every row a finite max.
       if (__builtin_amdgcn_ballot_w64((tmax - m_run) * c > 8.f) != 0) {
         const float m_new = fmaxf(m_run, tmax);  // raw-score units
-        const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
+        // (KMASK: a lane still without any real key has m_new = -inf; -inf - -inf would be NaN)
+        const float alpha = (KMASK && m_new == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f((m_run - m_new) * c);
         l_run *= alpha;
         o[0] *= alpha;
         o[1] *= alpha;
         m_run = m_new;
       }
-      const float mc = m_run * c;
+      // an all-masked row so far (KMASK only) has m = -inf: offset 0 gives P = 0, not NaN
+      const float mc = (KMASK && m_run == -INFINITY) ? 0.f : m_run * c;
       float psum = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
@@ -202,8 +230,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
   }
 
   if (q < T) {
-    const float inv_l = 1.f / l_run;
-    bf16_raw* dst = out + ((long)b * T + q) * H * kHD + (long)h * kHD;
+    // a row that never saw an unpadded key: O = 0 and lse = +inf (P = 0 in the backward)
+    const bool dead = KMASK && m_run == -INFINITY;
+    const float inv_l = dead ? 0.f : 1.f / l_run;
+    bf16_raw* dst = out + ((long)b * T + q) * H * hd + (long)h * hd;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) {
 #pragma unroll
@@ -211,26 +241,44 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
         ushort4_t v;
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = f2bf(o[dt][4 * g + i] * inv_l);
-        *reinterpret_cast<ushort4_t*>(dst + dt * 32 + 8 * g + 4 * half) = v;
+        const int d = dt * 32 + 8 * g + 4 * half;
+        if (!SMALLHD || d < hd) *reinterpret_cast<ushort4_t*>(dst + d) = v;
       }
     }
-    if (half == 0) lse[((long)b * H + h) * T + q] = (m_run * c + log2f(l_run)) * 0.6931471805599453f;
+    if (half == 0)
+      lse[((long)b * H + h) * T + q] = dead ? INFINITY : (m_run * c + log2f(l_run)) * 0.6931471805599453f;
   }
 }
 
 }  // namespace attn
 
-hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H, DropoutArgs dropout,
+template <bool DROPOUT, bool KMASK, bool SMALLHD>
+static void launch_fwd_variant(dim3 grid, hipStream_t stream, const bf16_raw* qkv, bf16_raw* out, float* lse,
+                               const AttnDims& d, int nqb, DropoutArgs dr) {
+  hipLaunchKernelGGL((attn::attn_fwd_kernel<DROPOUT, KMASK, SMALLHD>), grid, dim3(256), 0, stream, qkv, out, lse, d.T,
+                     d.H, nqb, dr, d.hd, d.scale * 1.4426950408889634f, d.key_bits);
+}
+
+hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, const AttnDims& d, DropoutArgs dropout,
                            hipStream_t stream) {
-  if (B <= 0 || T <= 0 || H <= 0 || T > 65535) return hipErrorInvalidValue;
-  const int nqb = (T + attn::kQBlk - 1) / attn::kQBlk;
-  dim3 grid(nqb, B * H);
-  if (dropout.thr != 0)
-    hipLaunchKernelGGL(attn::attn_fwd_kernel<true>, grid, dim3(256), 0, stream, (const bf16_raw*)qkv, (bf16_raw*)out,
-                       lse, T, H, nqb, dropout);
-  else
-    hipLaunchKernelGGL(attn::attn_fwd_kernel<false>, grid, dim3(256), 0, stream, (const bf16_raw*)qkv, (bf16_raw*)out,
-                       lse, T, H, nqb, dropout);
+  if (d.B <= 0 || d.T <= 0 || d.H <= 0 || d.T > 65535 || d.hd <= 0 || d.hd > attn::kHD || d.hd % 8 != 0)
+    return hipErrorInvalidValue;
+  const int nqb = (d.T + attn::kQBlk - 1) / attn::kQBlk;
+  dim3 grid(nqb, d.B * d.H);
+  const bool drop = dropout.thr != 0, km = d.key_bits != nullptr, small = d.hd != attn::kHD;
+  const int variant = (drop ? 4 : 0) | (km ? 2 : 0) | (small ? 1 : 0);
+  auto q = (const bf16_raw*)qkv;
+  auto o = (bf16_raw*)out;
+  switch (variant) {
+    case 0: launch_fwd_variant<false, false, false>(grid, stream, q, o, lse, d, nqb, dropout); break;
+    case 1: launch_fwd_variant<false, false, true>(grid, stream, q, o, lse, d, nqb, dropout); break;
+    case 2: launch_fwd_variant<false, true, false>(grid, stream, q, o, lse, d, nqb, dropout); break;
+    case 3: launch_fwd_variant<false, true, true>(grid, stream, q, o, lse, d, nqb, dropout); break;
+    case 4: launch_fwd_variant<true, false, false>(grid, stream, q, o, lse, d, nqb, dropout); break;
+    case 5: launch_fwd_variant<true, false, true>(grid, stream, q, o, lse, d, nqb, dropout); break;
+    case 6: launch_fwd_variant<true, true, false>(grid, stream, q, o, lse, d, nqb, dropout); break;
+    default: launch_fwd_variant<true, true, true>(grid, stream, q, o, lse, d, nqb, dropout); break;
+  }
   return hipGetLastError();
 }
 

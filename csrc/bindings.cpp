@@ -281,19 +281,42 @@ void embedding_bwd(const Tensor& dx, const Tensor& ids, Tensor dwte, Tensor dwpe
 }
 
 // ---- attention -------------------------------------------------------------------------------
-void check_qkv(const Tensor& qkv, int64_t B, int64_t T, int64_t H) {
+// head dim from the packed qkv [B*T, 3*H*hd]: a multiple of 8 up to 64 (the kernels' tiles are 64
+// wide; smaller heads are zero-filled in LDS/registers)
+int64_t attn_head_dim(const Tensor& qkv, int64_t B, int64_t T, int64_t H) {
   check_gpu(qkv, "qkv");
   check_dtype(qkv, at::kBFloat16, "qkv");
-  TORCH_CHECK(qkv.numel() == B * T * 3 * H * 64, "qkv must be [B*T, 3*H*64] (head_dim 64 only)");
+  TORCH_CHECK(B > 0 && T > 0 && H > 0 && qkv.numel() % (B * T * 3 * H) == 0, "qkv must be [B*T, 3*H*hd]");
+  const int64_t hd = qkv.numel() / (B * T * 3 * H);
+  TORCH_CHECK(hd % 8 == 0 && hd >= 8 && hd <= 64, "attention kernels need head_dim % 8 == 0 and 8 <= head_dim <= 64, got ",
+              hd);
+  return hd;
+}
+
+llmt::AttnDims attn_dims(int64_t B, int64_t T, int64_t H, int64_t hd) {
+  llmt::AttnDims d{};
+  d.B = (int)B;
+  d.T = (int)T;
+  d.H = (int)H;
+  d.hd = (int)hd;
+  d.scale = (float)(1.0 / std::sqrt((double)hd));
+  return d;
 }
 
 std::tuple<Tensor, Tensor> attn_fwd(const Tensor& qkv, int64_t B, int64_t T, int64_t H, double dropout_p,
-                                    int64_t dropout_seed) {
-  check_qkv(qkv, B, T, H);
+                                    int64_t dropout_seed, const c10::optional<Tensor>& key_bits) {
+  const int64_t hd = attn_head_dim(qkv, B, T, H);
   at::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
-  Tensor out = at::empty({B * T, H * 64}, qkv.options());
+  llmt::AttnDims dims = attn_dims(B, T, H, hd);
+  if (key_bits.has_value()) {
+    check_gpu(*key_bits, "key_bits");
+    check_dtype(*key_bits, at::kLong, "key_bits");
+    TORCH_CHECK(key_bits->numel() == B * ((T + 63) / 64), "key_bits must be [B, ceil(T/64)] int64");
+    dims.key_bits = reinterpret_cast<const uint64_t*>(key_bits->data_ptr<int64_t>());
+  }
+  Tensor out = at::empty({B * T, H * hd}, qkv.options());
   Tensor lse = at::empty({B, H, T}, qkv.options().dtype(at::kFloat));
-  check_hip(llmt::launch_attn_fwd(qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(), (int)B, (int)T, (int)H,
+  check_hip(llmt::launch_attn_fwd(qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(), dims,
                                   make_dropout(dropout_p, dropout_seed), cur_stream()),
             "attn_fwd");
   return {out, lse};
@@ -301,17 +324,25 @@ std::tuple<Tensor, Tensor> attn_fwd(const Tensor& qkv, int64_t B, int64_t T, int
 
 Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const Tensor& lse, int64_t B, int64_t T,
                 int64_t H, double dropout_p, int64_t dropout_seed, const c10::optional<Tensor>& dbias,
-                const c10::optional<Tensor>& delta_in) {
-  check_qkv(qkv, B, T, H);
+                const c10::optional<Tensor>& delta_in, const c10::optional<Tensor>& key_valid) {
+  const int64_t hd = attn_head_dim(qkv, B, T, H);
   for (const Tensor* t : {&dout, &out}) {
     check_gpu(*t, "dout/out");
     check_dtype(*t, at::kBFloat16, "dout/out");
-    TORCH_CHECK(t->numel() == B * T * H * 64, "dout/out must be [B*T, H*64]");
+    TORCH_CHECK(t->numel() == B * T * H * hd, "dout/out must be [B*T, H*hd]");
   }
   check_gpu(lse, "lse");
   check_dtype(lse, at::kFloat, "lse");
   TORCH_CHECK(lse.numel() == B * H * T, "lse must be [B, H, T]");
   at::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
+  llmt::AttnDims dims = attn_dims(B, T, H, hd);
+  if (key_valid.has_value()) {
+    check_gpu(*key_valid, "key_valid");
+    TORCH_CHECK(key_valid->scalar_type() == at::kByte || key_valid->scalar_type() == at::kBool,
+                "key_valid must be uint8/bool");
+    TORCH_CHECK(key_valid->numel() == B * T, "key_valid must be [B, T]");
+    dims.key_valid = reinterpret_cast<const uint8_t*>(key_valid->data_ptr());
+  }
   Tensor dqkv = at::empty_like(qkv);
   // delta_in: rowsum(dO * O) from the out-proj dX GEMM's epilogue (gemm_fused epilogue 3)
   Tensor delta;
@@ -328,12 +359,12 @@ Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const 
   if (dbias.has_value()) {
     check_gpu(*dbias, "dbias");
     check_dtype(*dbias, at::kFloat, "dbias");
-    TORCH_CHECK(dbias->numel() == 3 * H * 64, "dbias must have 3*H*64 elements");
+    TORCH_CHECK(dbias->numel() == 3 * H * hd, "dbias must have 3*H*hd elements");
     db = dbias->data_ptr<float>();
   }
   check_hip(llmt::launch_attn_bwd(dout.data_ptr(), qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
-                                  dqkv.data_ptr(), delta.data_ptr<float>(), dq.data_ptr<float>(), db, (int)B, (int)T,
-                                  (int)H, make_dropout(dropout_p, dropout_seed), cur_stream(), delta_in.has_value()),
+                                  dqkv.data_ptr(), delta.data_ptr<float>(), dq.data_ptr<float>(), db, dims,
+                                  make_dropout(dropout_p, dropout_seed), cur_stream(), delta_in.has_value()),
             "attn_bwd");
   return dqkv;
 }
@@ -501,9 +532,10 @@ TORCH_LIBRARY(llmtrain_hip, m) {
   m.def("embedding_fwd(Tensor ids, Tensor wte, Tensor wpe, float dropout_p=0., int dropout_seed=0) -> Tensor");
   m.def("embedding_bwd(Tensor dx, Tensor ids, Tensor(a!) dwte, Tensor(b!) dwpe, float dropout_p=0.,"
         " int dropout_seed=0) -> ()");
-  m.def("attn_fwd(Tensor qkv, int B, int T, int H, float dropout_p=0., int dropout_seed=0) -> (Tensor, Tensor)");
+  m.def("attn_fwd(Tensor qkv, int B, int T, int H, float dropout_p=0., int dropout_seed=0,"
+        " Tensor? key_bits=None) -> (Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, int B, int T, int H, float dropout_p=0.,"
-        " int dropout_seed=0, Tensor(a!)? dbias=None, Tensor? delta=None) -> Tensor");
+        " int dropout_seed=0, Tensor(a!)? dbias=None, Tensor? delta=None, Tensor? key_valid=None) -> Tensor");
   m.def("dropout_mask(int n, float p, int seed, Tensor like) -> Tensor");
   m.def("wgrad_gemm(Tensor dy, Tensor x, Tensor(a!) c, int split=0, int tile=0) -> ()");
   m.def("gemm_fused(Tensor a, Tensor b, bool b_kn, int epilogue, Tensor? bias=None, Tensor? u=None,"

@@ -131,21 +131,33 @@ struct GemmFusedArgs {
 };
 hipError_t launch_gemm_fused(const GemmFusedArgs& args, hipStream_t stream);
 
-// ---- causal flash attention (head_dim 64) ----------------------------------------------
-// qkv [B, T, 3, H, 64] bf16 (the packed projection output), out [B, T, H, 64] bf16,
+// ---- causal flash attention (head_dim <= 64, multiple of 8) ------------------------------
+// Shape + options shared by the forward and backward launchers.  The kernels are specialised for
+// head_dim 64 (GPT-2 124M/XL); any other multiple of 8 up to 64 (the reference presets' 32 and
+// 48) runs the same kernels with the missing head dims zero-filled in LDS/registers.  The optional
+// key-padding mask (reference models/gpt.py:60-64) excludes keys from the softmax; a query row
+// whose every causal key is masked gets O = 0 and lse = +inf (P = 0 in the backward).
+struct AttnDims {
+  int B = 0, T = 0, H = 0;
+  int hd = 64;                         // head dim
+  float scale = 0.125f;                // softmax scale, 1/sqrt(hd)
+  const uint64_t* key_bits = nullptr;  // fwd mask: [B, ceil(T/64)] words, bit j of word w = key 64w+j valid
+  const uint8_t* key_valid = nullptr;  // bwd mask: [B, T], nonzero = key valid
+};
+// qkv [B, T, 3, H, hd] bf16 (the packed projection output), out [B, T, H, hd] bf16,
 // lse [B, H, T] f32 (natural-log normaliser).
 // `dropout` masks the attention probabilities (element (b, h, q, k) of the site: plane seed
 // mix32(seed + (b*H + h) * 0x9E3779B9), index q*T + k); lse stays the undropped normaliser
-hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H,
-                           DropoutArgs dropout, hipStream_t stream);
-// dqkv [B, T, 3, H, 64] bf16; optional `dbias` [3*H*64] f32 accumulates the column sums of dqkv
+hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, const AttnDims& dims, DropoutArgs dropout,
+                           hipStream_t stream);
+// dqkv [B, T, 3, H, hd] bf16; optional `dbias` [3*H*hd] f32 accumulates the column sums of dqkv
 // (the qkv projection's bias gradient); `delta` [B, H, T] f32 and `dq_part`
 // (attn_bwd_workspace_floats(B, T, H) floats) scratch
 long attn_bwd_workspace_floats(int B, int T, int H);
 // delta_ready: `delta` already holds rowsum(dO * O) (the out-proj dX GEMM's epilogue 3, which
 // then also added the V part of `dbias`): the delta pass is skipped
 hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse,
-                           void* dqkv, float* delta, float* dq_part, float* dbias, int B, int T,
-                           int H, DropoutArgs dropout, hipStream_t stream, bool delta_ready = false);
+                           void* dqkv, float* delta, float* dq_part, float* dbias, const AttnDims& dims,
+                           DropoutArgs dropout, hipStream_t stream, bool delta_ready = false);
 
 }  // namespace llmt

@@ -166,17 +166,21 @@ class GPT(nn.Module):
     # -- fused path ------------------------------------------------------------------------
 
     def fused_supported(self, device_type: str = "cuda") -> bool:
-        """Whether the fused engine covers this shape on ``device_type``.  On the GPU the kernels
-        need head_dim 64 (the flash-attention specialisation, SURVEY §2.2 N1 — GPT-2 124M and XL
-        both use it) and LayerNorm widths d % 4 == 0, d <= 2048; other shapes train on the module
-        path.  On CPU the engine runs the reference ops, which take any shape.  Dropout is
-        supported everywhere (counter-based masks fused into the embedding, add+LayerNorm and
-        flash-attention kernels)."""
+        """Whether the fused engine covers this shape on ``device_type``.  On the GPU the
+        flash-attention kernels take head dims that are multiples of 8 up to 64 (64 is the fast
+        specialisation — GPT-2 124M and XL; the reference presets' 32 and 48 run zero-filled in
+        the same tiles) and key-padding masks; LayerNorm widths need d % 4 == 0,
+        d <= 2048.  Other shapes train on the module path.  On CPU the engine runs the reference
+        ops, which take any shape.  Dropout is supported everywhere (counter-based masks fused into
+        the embedding, add+LayerNorm and flash-attention kernels)."""
         if device_type != "cuda":
             return True
+        if self.d_model % self.n_heads != 0:
+            return False
+        hd = self.d_model // self.n_heads
         return (
-            self.d_model % self.n_heads == 0
-            and self.d_model // self.n_heads == 64
+            hd % 8 == 0
+            and 8 <= hd <= 64
             and self.d_model % 4 == 0
             and self.d_model <= 2048
             and self.d_ff % 8 == 0

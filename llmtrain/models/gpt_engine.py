@@ -118,6 +118,10 @@ class _StepState:
     dlogits: torch.Tensor | None = None
     drop_p: float = 0.0
     drop_seed: int = 0
+    # key-padding mask (reference gpt.py:60-64, 73-74): the attention kernels' key masks and the
+    # [M, 1] row keep-factor that zeroes the attention branch of padded query positions
+    key_masks: tuple[torch.Tensor, torch.Tensor] | None = None
+    keep_col: torch.Tensor | None = None
 
     def site(self, k: int) -> tuple[float, int]:
         """``(p, site_seed)`` of dropout site ``k`` for this forward (``(0, 0)`` = off)."""
@@ -151,6 +155,7 @@ class FusedGPTEngine:
         self.compute_dtype = compute_dtype
         self.blocks = list(model.blocks)
         self.n_heads = model.n_heads
+        self.head_dim = model.d_model // model.n_heads
         self.vocab = model.vocab_size
         self.eps = model.ln_f.eps
         for blk in self.blocks:
@@ -181,7 +186,6 @@ class FusedGPTEngine:
         self.segment_order = [name for name, _ in groups]
         self.store = FlatParamStore(groups, shadow_dtype=compute_dtype, pad_last_rows=VOCAB_PAD)
         self.grad_ready: Callable[[str], None] | None = None
-        self.padding_seen = torch.zeros((), dtype=torch.bool, device=self.store.device)
         self._anchor = torch.zeros((), requires_grad=True, device=self.store.device)
         self.wgrad_impl = os.environ.get("LLMTRAIN_WGRAD", "hip")
         # weight-gradient GEMMs on a second HIP stream, overlapping the dX GEMMs and the
@@ -314,11 +318,12 @@ class FusedGPTEngine:
             state.drop_seed = int(torch.randint(0, 2**31 - 1, (1,)).item())
 
         if mask is not None:
-            # The fused attention has no key-padding path: record padded batches on-device and
-            # let the trainer raise at its next sync point (no per-step host sync here).
-            self.padding_seen |= ~mask.bool().all()
+            # key padding (no host sync: a mask is taken as given; the trainer drops all-ones masks
+            # on the host before they reach the device)
             row_w = mask.reshape(-1).float()
             row_w = row_w / row_w.sum().clamp_min(1.0)
+            state.key_masks = ops.attn_key_masks(mask)
+            state.keep_col = mask.reshape(-1, 1).to(cdt)
         else:
             row_w = torch.full((n_tok,), 1.0 / n_tok, dtype=torch.float32, device=ids.device)
 
@@ -332,8 +337,12 @@ class FusedGPTEngine:
                 x, delta, blk.ln_1.weight, blk.ln_1.bias, self.eps, cdt, dropout=state.site(3 * i)
             )  # site 3i = the previous block's MLP branch (unused for block 0: delta is None)
             qkv = self._linear(h1, blk.attn.qkv_proj, fused=True)
-            att, lse = ops.attn_fwd(qkv, bsz, seqlen, self.n_heads, dropout=state.site(2 + 3 * i))
+            att, lse = ops.attn_fwd(
+                qkv, bsz, seqlen, self.n_heads, dropout=state.site(2 + 3 * i), key_masks=state.key_masks
+            )
             y = self._linear(att, blk.attn.out_proj, fused=True)
+            if state.keep_col is not None:  # padded query rows add nothing to the residual stream
+                y = y * state.keep_col
             xm, h2, mu2, rs2 = ops.add_layernorm_fwd(
                 xs, y, blk.ln_2.weight, blk.ln_2.bias, self.eps, cdt, dropout=state.site(1 + 3 * i)
             )
@@ -439,11 +448,16 @@ class FusedGPTEngine:
             self._wgrad(self._g(blk.mlp_fc.weight), du, a.h2)
             dh2 = torch.mm(du, self._w(blk.mlp_fc.weight))
             del du
+            masked = st.keep_col is not None
             dxm, dy_lp = ops.layernorm_bwd(
                 dh2, a.xm, a.mu2, a.rs2, blk.ln_2.weight, dx, self._g(blk.ln_2.weight), self._g(blk.ln_2.bias),
-                None, want_lowp=True, dproj_bias=self._g(blk.attn.out_proj.bias), dropout=st.site(1 + 3 * i),
+                None, want_lowp=True, dproj_bias=None if masked else self._g(blk.attn.out_proj.bias),
+                dropout=st.site(1 + 3 * i),
             )
             del dh2, dx, dx_lp
+            if masked:  # gradient of y * keep: padded rows feed nothing back into the attention
+                dy_lp = dy_lp * st.keep_col
+                ops.colsum_accum(dy_lp, self._g(blk.attn.out_proj.bias))
             # attention output projection
             self._wgrad(self._g(blk.attn.out_proj.weight), dy_lp, a.att)
             wo = self._w(blk.attn.out_proj.weight)
@@ -456,7 +470,8 @@ class FusedGPTEngine:
                 # (not taken -> delta None: attn_bwd computes it and the V-bias part itself)
                 d = qkv_bg.numel() // 3
                 datt, delta = ops.linear_dx_attn(
-                    dy_lp, wo, a.att, seqlen, v_bias_grad=qkv_bg[2 * d :] if attn_drop[0] == 0 else None
+                    dy_lp, wo, a.att, seqlen, v_bias_grad=qkv_bg[2 * d :] if attn_drop[0] == 0 else None,
+                    head_dim=self.head_dim,
                 )
             else:
                 datt = torch.mm(dy_lp, wo)
@@ -464,7 +479,7 @@ class FusedGPTEngine:
             # the qkv-bias gradient (column sums of dqkv) is fused into the attention backward
             dqkv = ops.attn_bwd(
                 datt, a.qkv, a.att, a.lse, bsz, seqlen, self.n_heads, dropout=attn_drop,
-                qkv_bias_grad=qkv_bg, delta=delta,
+                qkv_bias_grad=qkv_bg, delta=delta, key_masks=st.key_masks,
             )
             del datt
             self._wgrad(self._g(blk.attn.qkv_proj.weight), dqkv, a.h1)

@@ -20,6 +20,7 @@ __all__ = [
     "add_layernorm_fwd",
     "attn_bwd",
     "attn_fwd",
+    "attn_key_masks",
     "colsum_accum",
     "cross_entropy_fwd_bwd",
     "embedding_bwd",
@@ -129,24 +130,44 @@ def embedding_bwd(dx, ids, dwte, dwpe, dropout=(0.0, 0)) -> None:
         ref.embedding_bwd(dx, ids, dwte, dwpe, p, seed)
 
 
-def attn_fwd(qkv, bsz: int, seqlen: int, n_heads: int, dropout=(0.0, 0)):
+def attn_key_masks(mask: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Device forms of a ``[B, T]`` key-padding mask for the attention kernels: ``key_bits``
+    ``[B, ceil(T/64)]`` int64 (bit j of word w = key 64w + j is valid; the forward reads one word
+    per 64-key tile) and ``key_valid`` ``[B, T]`` uint8 (the backward reads its lane's key)."""
+    bsz, seqlen = mask.shape
+    valid = mask.bool()
+    words = -(-seqlen // 64)
+    padded = torch.zeros(bsz, words * 64, dtype=torch.int64, device=mask.device)
+    padded[:, :seqlen] = valid.to(torch.int64)
+    shifts = torch.arange(64, dtype=torch.int64, device=mask.device)
+    bits = (padded.view(bsz, words, 64) << shifts).sum(dim=-1)  # wraps into bit 63 as int64
+    return bits.contiguous(), valid.to(torch.uint8).contiguous()
+
+
+def attn_fwd(qkv, bsz: int, seqlen: int, n_heads: int, dropout=(0.0, 0), key_masks=None):
+    """Causal flash attention over packed ``qkv``; ``key_masks`` = :func:`attn_key_masks` of the
+    batch's key-padding mask (None = every key valid)."""
     p, seed = dropout
     if _on_gpu(qkv):
-        return hip_ops().attn_fwd(qkv, bsz, seqlen, n_heads, p, seed)
-    return ref.attn_fwd(qkv, bsz, seqlen, n_heads, p, seed)
+        bits = None if key_masks is None else key_masks[0]
+        return hip_ops().attn_fwd(qkv, bsz, seqlen, n_heads, p, seed, bits)
+    valid = None if key_masks is None else key_masks[1]
+    return ref.attn_fwd(qkv, bsz, seqlen, n_heads, p, seed, valid)
 
 
 def attn_bwd(
-    dout, qkv, out, lse, bsz: int, seqlen: int, n_heads: int, dropout=(0.0, 0), qkv_bias_grad=None, delta=None
+    dout, qkv, out, lse, bsz: int, seqlen: int, n_heads: int, dropout=(0.0, 0), qkv_bias_grad=None, delta=None,
+    key_masks=None,
 ):
     """Attention backward -> packed ``dqkv``; ``qkv_bias_grad`` (fp32 ``[3d]``), when given,
     accumulates ``colsum(dqkv)`` (fused into the kernels on GPU).  ``delta`` (GPU): the row
     constants ``rowsum(dO * O)`` already computed by :func:`linear_dx_attn`, which then also added
     the V part of ``qkv_bias_grad`` when there is no dropout; the delta pass is skipped."""
     p, seed = dropout
+    valid = None if key_masks is None else key_masks[1]
     if _on_gpu(dout):
-        return hip_ops().attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads, p, seed, qkv_bias_grad, delta)
-    dqkv = ref.attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads, p, seed)
+        return hip_ops().attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads, p, seed, qkv_bias_grad, delta, valid)
+    dqkv = ref.attn_bwd(dout, qkv, out, lse, bsz, seqlen, n_heads, p, seed, valid)
     if qkv_bias_grad is not None:
         ref.colsum_accum(dqkv, qkv_bias_grad)
     return dqkv
@@ -214,7 +235,7 @@ def linear_dx_gelu_bwd(dy, w, u, dbias=None):
     return gelu_bwd(torch.mm(dy, w), u, dbias)
 
 
-def linear_dx_attn(dy, w, att, seqlen: int, v_bias_grad=None):
+def linear_dx_attn(dy, w, att, seqlen: int, v_bias_grad=None, head_dim: int = 64):
     """Data gradient of the attention output projection, ``dO = dy @ w``, plus the flash-attention
     backward's row constants ``delta[b, h, t] = sum_d dO * O`` (``att`` = the attention output O)
     and, when given, ``v_bias_grad += colsum(dO)`` (the V part of the qkv bias gradient, valid
@@ -226,6 +247,7 @@ def linear_dx_attn(dy, w, att, seqlen: int, v_bias_grad=None):
         ATTN_DX_FUSED
         and _on_gpu(dy)
         and dy.dtype == torch.bfloat16
+        and head_dim == 64  # the epilogue's per-head row dots are 64 columns wide
         and dy.shape[0] % seqlen == 0
         and w.shape[1] % 64 == 0
         and _fgemm_ok(dy, dy.shape[1], w.shape[1], w, att, op="dx_attn")

@@ -233,19 +233,36 @@ def _split_qkv(qkv: torch.Tensor, bsz: int, seqlen: int, n_heads: int):
     return q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
 
 
-def attn_fwd(
-    qkv: torch.Tensor, bsz: int, seqlen: int, n_heads: int, dropout_p: float = 0.0, dropout_seed: int = 0
-) -> tuple[torch.Tensor, torch.Tensor]:
-    """Causal attention over packed ``qkv`` ``[B*T, 3d]`` with optional probability dropout.
+def _attn_masks(bsz: int, seqlen: int, device: torch.device, key_valid: torch.Tensor | None) -> torch.Tensor:
+    """``[B or 1, 1, T, T]`` bool: True where a score is masked (future key, or padded key)."""
+    masked = torch.ones(seqlen, seqlen, dtype=torch.bool, device=device).triu(1)[None, None]
+    if key_valid is not None:
+        masked = masked | ~key_valid.bool().view(bsz, 1, 1, seqlen)
+    return masked
 
-    Returns ``out`` ``[B*T, d]`` (dtype of qkv) and ``lse`` ``[B, H, T]`` fp32 (undropped).
+
+def attn_fwd(
+    qkv: torch.Tensor,
+    bsz: int,
+    seqlen: int,
+    n_heads: int,
+    dropout_p: float = 0.0,
+    dropout_seed: int = 0,
+    key_valid: torch.Tensor | None = None,
+) -> tuple[torch.Tensor, torch.Tensor]:
+    """Causal attention over packed ``qkv`` ``[B*T, 3d]`` with optional probability dropout and
+    key-padding mask ``key_valid`` ``[B, T]`` (reference ``models/gpt.py:56-69``).
+
+    Returns ``out`` ``[B*T, d]`` (dtype of qkv) and ``lse`` ``[B, H, T]`` fp32 (undropped).  A
+    query row with no unmasked key gets ``out = 0`` and ``lse = +inf`` (it is a padded position,
+    whose branch output the caller zeroes anyway — reference ``gpt.py:73-74``).
     """
     q, k, v = (t.float() for t in _split_qkv(qkv, bsz, seqlen, n_heads))
     hd = q.shape[-1]
     s = (q @ k.transpose(-2, -1)) / math.sqrt(hd)
-    causal = torch.ones(seqlen, seqlen, dtype=torch.bool, device=qkv.device).triu(1)
-    s = s.masked_fill(causal, float("-inf"))
+    s = s.masked_fill(_attn_masks(bsz, seqlen, qkv.device, key_valid), float("-inf"))
     lse = torch.logsumexp(s, dim=-1)
+    lse = torch.where(torch.isfinite(lse), lse, torch.full_like(lse, float("inf")))
     p = torch.exp(s - lse[..., None])
     thr, dscale = dropout_params(dropout_p)
     if thr:
@@ -265,6 +282,7 @@ def attn_bwd(
     n_heads: int,
     dropout_p: float = 0.0,
     dropout_seed: int = 0,
+    key_valid: torch.Tensor | None = None,
 ) -> torch.Tensor:
     """Gradient of :func:`attn_fwd` w.r.t. packed ``qkv``; returns ``[B*T, 3d]`` in qkv dtype."""
     q, k, v = (t.float() for t in _split_qkv(qkv, bsz, seqlen, n_heads))
@@ -273,8 +291,7 @@ def attn_bwd(
     do = dout.float().view(bsz, seqlen, n_heads, hd).transpose(1, 2)
     o = out.float().view(bsz, seqlen, n_heads, hd).transpose(1, 2)
     s = (q @ k.transpose(-2, -1)) * scale
-    causal = torch.ones(seqlen, seqlen, dtype=torch.bool, device=qkv.device).triu(1)
-    p = torch.exp(s - lse[..., None]).masked_fill(causal, 0.0)
+    p = torch.exp(s - lse[..., None]).masked_fill(_attn_masks(bsz, seqlen, qkv.device, key_valid), 0.0)
     thr, dscale = dropout_params(dropout_p)
     keep = attn_dropout_keep(dropout_seed, dropout_p, bsz, n_heads, seqlen, qkv.device) if thr else None
     pd = p if keep is None else torch.where(keep, p * dscale, torch.zeros_like(p))

@@ -86,8 +86,28 @@ def lr_lambda_factory(warmup_steps: int, max_steps: int):  # type: ignore[no-unt
     return lr_lambda
 
 
+def _drop_dense_mask(batch: dict[str, Any]) -> dict[str, Any]:
+    """Drop an all-ones ``attention_mask`` while the batch is still on the host (a cheap CPU check,
+    no device sync): without padding the masked mean IS the plain mean, and the fused engine /
+    SDPA then take their unmasked kernels.  Malformed masks are kept so the adapter's validation
+    still rejects them (reference ``models/gpt.py:221-252``)."""
+    mask = batch.get("attention_mask")
+    ids = batch.get("input_ids")
+    if (
+        torch.is_tensor(mask)
+        and torch.is_tensor(ids)
+        and mask.device.type == "cpu"
+        and mask.dtype in (torch.bool, torch.long)
+        and mask.shape == ids.shape
+        and bool(mask.all())
+    ):
+        return {k: v for k, v in batch.items() if k != "attention_mask"}
+    return batch
+
+
 def _to_device(batch: dict[str, Any], device: torch.device) -> dict[str, Any]:
     non_blocking = device.type == "cuda"
+    batch = _drop_dense_mask(batch)
     return {
         k: v.to(device, non_blocking=non_blocking) if torch.is_tensor(v) else v for k, v in batch.items()
     }
@@ -358,14 +378,6 @@ class Trainer:
         self._optimizer_step()
         return step_loss / accum, tokens
 
-    def _check_engine_flags(self) -> None:
-        engine = getattr(self._raw_model, "engine", None)
-        if engine is not None and bool(engine.padding_seen.item()):
-            raise RuntimeError(
-                "fused GPT engine received a batch with attention_mask zeros; key-padding is not "
-                "implemented on the fused path (set model.extra.fused=false)"
-            )
-
     def _profiler(self) -> Any:
         spec = self._cfg.trainer.extra.get("profile")
         if not spec or self._run_dir is None or not self._is_main:
@@ -452,7 +464,6 @@ class Trainer:
 
             if step % cfg.log_every_steps == 0 or step == max_steps:
                 avg_loss = float(interval_loss.item()) / interval_steps  # the interval's one sync
-                self._check_engine_flags()
                 interval_time = time.perf_counter() - interval_t0
                 step_time = interval_time / interval_steps
                 tps = interval_tokens / interval_time if interval_time > 0 else 0.0

@@ -46,11 +46,31 @@ def test_fused_masked_loss_matches_masked_mean() -> None:
     with torch.no_grad():
         loss = fused.fused_loss(ids, ids, mask)
     assert abs(loss.item() - loss_ref.item()) < 1e-5
-    assert not bool(fused.engine.padding_seen)
-    mask[0, 3] = 0
-    with torch.no_grad():
-        fused.fused_loss(ids, ids, mask)
-    assert bool(fused.engine.padding_seen)
+
+
+@pytest.mark.parametrize("n_heads", [4, 2])  # head dims 16 and 32
+def test_fused_key_padding_matches_module_path(n_heads: int) -> None:
+    """Key-padding mask (reference gpt.py:60-64 key masking + :73-74 zeroing of padded query rows)
+    on the fused engine: loss and every gradient equal the module path's autograd, with left and
+    right padding (rows whose keys are all padded included)."""
+    ref, fused = _pair(n_heads=n_heads)
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(0, 100, (3, 16), generator=g)
+    labels = torch.randint(0, 100, (3, 16), generator=g)
+    mask = torch.ones(3, 16, dtype=torch.long)
+    mask[0, 11:] = 0  # right padding
+    mask[1, :5] = 0   # left padding: queries 0..4 see no valid key
+    mask[2, 7] = 0    # a hole
+    logits = ref(ids, attention_mask=mask)
+    keep = mask.reshape(-1).bool()
+    loss_ref = F.cross_entropy(logits.reshape(-1, 100), labels.reshape(-1), reduction="none")[keep].mean()
+    loss_ref.backward()
+    fused.flat_store.zero_grad()
+    loss = fused.fused_loss(ids, labels, mask)
+    loss.backward()
+    assert abs(loss.item() - loss_ref.item()) < 1e-5
+    for (name, p), (_, q) in zip(fused.named_parameters(), ref.named_parameters()):
+        torch.testing.assert_close(p.grad, q.grad, atol=1e-6, rtol=1e-4, msg=name)
 
 
 def test_gradient_accumulation_and_views() -> None:

@@ -49,6 +49,57 @@ def test_fused_matches_module_path(gpu_device):
     print("worst relative grad error", worst)
 
 
+# the reference presets' model shapes: V, block, d, L, H, F
+PRESET_SHAPES = {
+    "gpt_smoke": (16, 8, 64, 2, 2, 128),  # head dim 32
+    "k8s_configmap": (50257, 128, 256, 6, 8, 1024),  # head dim 32
+    "gpt_wikitext_ddp": (50257, 128, 256, 4, 4, 1024),  # head dim 64
+    "gpt_wikitext_better": (50257, 256, 384, 12, 8, 1536),  # head dim 48
+}
+
+
+@pytest.mark.parametrize("preset", sorted(PRESET_SHAPES))
+@pytest.mark.parametrize("padded", [False, True])
+def test_fused_engine_covers_reference_presets(gpu_device, preset, padded):
+    """Every reference preset's model trains on the fused engine on GPU (``fused_supported``), and
+    its bf16 loss and gradients track fp32 autograd of the module path — with key-padding masks
+    (reference gpt.py:60-64, 73-74) too."""
+    V, block, d, L, H, F_ = PRESET_SHAPES[preset]
+    torch.manual_seed(0)
+    ref_model = GPT(vocab_size=V, block_size=block, d_model=d, n_layers=L, n_heads=H, d_ff=F_, dropout=0.0)
+    ref_model = ref_model.to(gpu_device)
+    assert ref_model.fused_supported("cuda")
+    fused = copy.deepcopy(ref_model)
+    engine = fused.prepare_runtime(compute_dtype=torch.bfloat16)
+    B = 4
+    g = torch.Generator(device="cpu").manual_seed(1)
+    ids = torch.randint(0, V, (B, block), generator=g).to(gpu_device)
+    labels = torch.randint(0, V, (B, block), generator=g).to(gpu_device)
+    mask = None
+    if padded:
+        mask = torch.ones(B, block, dtype=torch.long)
+        mask[0, block - block // 3 :] = 0
+        mask[1, : block // 4 + 1] = 0
+        mask[2, block // 2] = 0
+        mask = mask.to(gpu_device)
+
+    logits = ref_model(ids, attention_mask=mask)
+    per_tok = F.cross_entropy(logits.reshape(-1, V).float(), labels.reshape(-1), reduction="none")
+    loss_ref = per_tok.mean() if mask is None else per_tok[mask.reshape(-1).bool()].mean()
+    loss_ref.backward()
+    engine.store.zero_grad()
+    loss = fused.fused_loss(ids, labels, mask)
+    loss.backward()
+    assert abs(loss.item() - loss_ref.item()) < 1e-2 * max(1.0, abs(loss_ref.item()))
+    worst = 0.0
+    for (name, p), (_, q) in zip(fused.named_parameters(), ref_model.named_parameters()):
+        num = (p.grad - q.grad).norm().item()
+        den = q.grad.norm().item() + 1e-12
+        worst = max(worst, num / den)
+        assert num / den < 3e-2, f"{name}: relative grad error {num / den:.3e}"
+    print(f"{preset} padded={padded}: worst relative grad error {worst:.2e}")
+
+
 def test_fused_no_grad_eval_matches(gpu_device):
     model = _model(gpu_device)
     model.prepare_runtime(compute_dtype=torch.bfloat16)

@@ -4,12 +4,18 @@ NPROC ?= 8
 GPURUN ?= /usr/local/graft/bin/gpurun
 
 .PHONY: build test test-gpu bench bench-module profile parity train-smoke train-ddp train-gpt2 train-gpt2-ddp8 \
-        generate mlflow k8s-build k8s-train k8s-logs k8s-clean k8s-e2e lint \
+        generate mlflow format k8s-build k8s-train k8s-logs k8s-clean k8s-e2e lint \
         k8s-kind-cluster k8s-kind-delete k8s-kind-smoke k8s-mlflow \
         k8s-dashboard k8s-dashboard-token k8s-dashboard-proxy k8s-dashboard-delete
 
 build:                 ## compile every HIP kernel for gfx950 into llmtrain/ops/_llmtrain_hip.so
 	$(PY) -m llmtrain.ops.build
+
+lint:                  ## ruff + mypy when installed, plus the built-in checker (scripts/lint.py)
+	$(PY) scripts/lint.py
+
+format:                ## ruff format (when installed)
+	$(PY) -m ruff format llmtrain tests bench scripts examples bench.py __graft_entry__.py
 
 test:                  ## CPU test suite (contracts, fused engine on CPU, multi-process gloo DDP)
 	$(PY) -m pytest tests -m "not gpu" -q

@@ -135,7 +135,9 @@ def fgemm_one(K: int, N: int, epi: int = 0, b_kn: bool = False, M: int = 65536, 
     bias = torch.randn(N, device=dev, dtype=torch.bfloat16)
     u = torch.randn(M, N, device=dev, dtype=torch.bfloat16)
     db = torch.zeros(N, device=dev)
-    fn = lambda: ops.gemm_fused(x, w, b_kn, epi, None if epi == 2 else bias, u if epi == 2 else None, db if epi == 2 else None)  # noqa: E731
+    fn = lambda: ops.gemm_fused(  # noqa: E731
+        x, w, b_kn, epi, None if epi == 2 else bias, u if epi == 2 else None, db if epi == 2 else None
+    )
     ms = timeit(fn, iters=reps)
     print(json.dumps({"K": K, "N": N, "epi": epi, "b_kn": b_kn, "ms": round(ms, 4),
                       "TFLOPs": round(2.0 * M * K * N / ms / 1e9, 1)}), flush=True)

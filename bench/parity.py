@@ -59,7 +59,8 @@ def run_path(path: str, args: argparse.Namespace) -> dict:
                  "extra": {"train_sequences": args.steps * args.micro_batch, "val_sequences": args.val_sequences,
                            "branching": args.branching}},
         "trainer": {"max_steps": args.steps, "micro_batch_size": args.micro_batch, "grad_accum_steps": 1,
-                    "lr": args.lr, "weight_decay": 0.1, "warmup_steps": args.warmup if args.warmup is not None else max(1, args.steps // 3),
+                    "lr": args.lr, "weight_decay": 0.1,
+                    "warmup_steps": args.warmup if args.warmup is not None else max(1, args.steps // 3),
                     "max_grad_norm": 1.0, "log_every_steps": max(1, args.steps // 5),
                     "eval_every_steps": args.steps, "save_every_steps": 10**9},
         "ddp": {"enabled": False}, "mlflow": {"enabled": False},

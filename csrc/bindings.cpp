@@ -482,7 +482,8 @@ Tensor sumsq(const Tensor& x) {
 void adamw_flat(Tensor param, const Tensor& grad, Tensor exp_avg, Tensor exp_avg_sq, const c10::optional<Tensor>& shadow,
                 double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
                 const c10::optional<Tensor>& grad_scale) {
-  for (const Tensor* t : {static_cast<const Tensor*>(&param), &grad, static_cast<const Tensor*>(&exp_avg), static_cast<const Tensor*>(&exp_avg_sq)}) {
+  for (const Tensor* t : {static_cast<const Tensor*>(&param), &grad, static_cast<const Tensor*>(&exp_avg),
+                          static_cast<const Tensor*>(&exp_avg_sq)}) {
     check_gpu(*t, "adamw buffer");
     check_dtype(*t, at::kFloat, "adamw buffer");
     TORCH_CHECK(t->numel() == param.numel(), "adamw buffers must have equal numel");

@@ -41,7 +41,6 @@ Reference call sites replaced: ``models/gpt.py:49-74`` (attention), ``:86-105`` 
 
 from __future__ import annotations
 
-import contextlib
 import os
 from collections.abc import Callable
 from dataclasses import dataclass, field

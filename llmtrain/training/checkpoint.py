@@ -7,7 +7,8 @@ Payload keys (the 6-key contract): ``step``, ``model_state_dict`` (fp32 master w
 resume metadata (world size, data position); readers that do not know it ignore it.
 
 Improvements over the reference: writes are atomic (``.tmp`` + ``os.replace``; a crash never
-leaves a truncated "latest" file, SURVEY §5.2) and loading always uses the safe ``weights_only=True`` unpickler (never arbitrary code);
+leaves a truncated "latest" file) and loading always uses the safe ``weights_only=True``
+unpickler (never arbitrary code);
 the numpy types a reference checkpoint stores in ``rng_states["numpy"]`` are allow-listed
 explicitly so reference checkpoints still load.
 """

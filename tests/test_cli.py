@@ -30,7 +30,9 @@ def _write(tmp: Path, **over) -> Path:  # type: ignore[no-untyped-def]
 
 def _run(*args: str, cwd: Path) -> subprocess.CompletedProcess[str]:
     env = dict(os.environ, PYTHONPATH=str(REPO))
-    return subprocess.run([sys.executable, "-m", "llmtrain", *args], cwd=cwd, env=env, capture_output=True, text=True, timeout=300)
+    return subprocess.run(
+        [sys.executable, "-m", "llmtrain", *args], cwd=cwd, env=env, capture_output=True, text=True, timeout=300
+    )
 
 
 def test_help_and_version(in_tmp: Path) -> None:

@@ -279,7 +279,9 @@ def test_gemm_fused_dgelu(gpu_device, M, N, K, b_kn):
     _close(dbias, 0.5 + du.float().sum(0), 1e-3, 1e-4, "dbias")
 
 
-@pytest.mark.parametrize("M,N,K,T", [(4096, 768, 768, 1024), (1536, 768, 768, 512), (600, 256, 256, 300), (2048, 1600, 1600, 256)])
+@pytest.mark.parametrize(
+    "M,N,K,T", [(4096, 768, 768, 1024), (1536, 768, 768, 512), (600, 256, 256, 300), (2048, 1600, 1600, 256)]
+)
 @pytest.mark.parametrize("b_kn", [True, False])
 def test_gemm_fused_attn_dx_delta(gpu_device, M, N, K, T, b_kn):
     """Epilogue 3: dO = dY @ W plus the attention backward's delta = per-head rowsum(dO * O) and

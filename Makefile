@@ -4,7 +4,7 @@ NPROC ?= 8
 GPURUN ?= /usr/local/graft/bin/gpurun
 
 .PHONY: build test test-gpu bench bench-module profile parity train-smoke train-ddp train-gpt2 train-gpt2-ddp8 \
-        generate mlflow format k8s-build k8s-train k8s-logs k8s-clean k8s-e2e lint \
+        generate mlflow format k8s-build k8s-train k8s-logs k8s-clean k8s-e2e k8s-e2e-cpu k8s-train-resilient lint \
         k8s-kind-cluster k8s-kind-delete k8s-kind-smoke k8s-mlflow \
         k8s-dashboard k8s-dashboard-token k8s-dashboard-proxy k8s-dashboard-delete
 
@@ -70,6 +70,13 @@ k8s-clean:
 k8s-e2e:
 	bash k8s/test_e2e.sh
 
+k8s-train-resilient:   ## the Job under the gang-restart controller (fail fast, restart all ranks, resume)
+	kubectl apply -f k8s/rbac.yaml -f k8s/storage.yaml -f k8s/configmap.yaml -f k8s/service.yaml
+	bash k8s/gang_restart.sh --job k8s/job.yaml --max-restarts 3
+
+k8s-e2e-cpu:           ## kind: create/reuse cluster, build+load image, 2-pod gloo Job with one injected crash
+	bash k8s/test_e2e.sh --cpu --inject-failure
+
 # ---- local kind cluster: CPU smoke of the same IndexedJob plumbing (gloo, 2 pods) -------------
 DASHBOARD_URL ?= https://raw.githubusercontent.com/kubernetes/dashboard/v2.7.0/aio/deploy/recommended.yaml
 
@@ -82,7 +89,7 @@ k8s-kind-delete:
 
 k8s-kind-smoke: k8s-build
 	kind load docker-image llmtrain-mi355x:dev --name llmtrain
-	kubectl apply -f k8s/rbac.yaml -f k8s/storage.yaml -f k8s/kind/configmap-cpu.yaml -f k8s/service.yaml -f k8s/kind/job-cpu.yaml
+	kubectl apply -f k8s/rbac.yaml -f k8s/kind/storage-kind.yaml -f k8s/kind/configmap-cpu.yaml -f k8s/service.yaml -f k8s/kind/job-cpu.yaml
 	kubectl wait --for=condition=complete --timeout=600s job/llmtrain
 
 k8s-mlflow:

@@ -17,7 +17,8 @@ What changes on the MI355X path:
 * resume replays the data order on every rank (each rank skips its own shard's batches — the
   reference disables replay under DDP);
 * ``peak_memory`` reports ``torch.cuda.max_memory_allocated`` (GiB) on GPU;
-* optional ``trainer.extra``: ``keep_last_k``, ``fail_at_step`` (fault injection),
+* optional ``trainer.extra``: ``keep_last_k``, ``fail_at_step`` / ``fail_rank`` (fault injection:
+  that rank raises at that step of a run that did not resume — one simulated crash per job),
   ``profile`` (torch.profiler window), ``bucket_cap_mb``, ``grad_reduce_dtype``;
 * ``train/allreduce_ms`` (max over ranks) logs the exposed gradient all-reduce time of the flat
   reducer — the part of the communication NOT hidden behind the backward.
@@ -378,6 +379,11 @@ class Trainer:
         self._optimizer_step()
         return step_loss / accum, tokens
 
+    def _fault_rank(self) -> bool:
+        """``trainer.extra.fail_rank`` (default: every rank) picks the rank that crashes."""
+        target = self._cfg.trainer.extra.get("fail_rank")
+        return target is None or int(target) == self._rank
+
     def _profiler(self) -> Any:
         spec = self._cfg.trainer.extra.get("profile")
         if not spec or self._run_dir is None or not self._is_main:
@@ -445,8 +451,9 @@ class Trainer:
             if profiler is not None:
                 profiler.before_step(step)
             step_loss_dev, step_tokens = self.train_step(batches)
-            if fail_at is not None and step == int(fail_at):
-                raise RuntimeError(f"fault injection: trainer.extra.fail_at_step={fail_at}")
+            if fail_at is not None and step == int(fail_at) and resumed_from_step is None and self._fault_rank():
+                # simulated crash of one incarnation of the job: a resumed run does not re-fire it
+                raise RuntimeError(f"fault injection: trainer.extra.fail_at_step={fail_at} (rank {self._rank})")
             last_step_loss_dev = step_loss_dev
             tokens_local_total += step_tokens
             if step == 1:

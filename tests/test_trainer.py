@@ -108,6 +108,21 @@ def test_tracker_injection_params_once_and_metric_steps() -> None:
 def test_fault_injection_and_nan_guard() -> None:
     with pytest.raises(RuntimeError, match="fault injection"):
         Trainer(_cfg(extra={"fail_at_step": 2})).fit()
+    Trainer(_cfg(extra={"fail_at_step": 2, "fail_rank": 1})).fit()  # only rank 1 crashes
     trainer = Trainer(_cfg(lr=1e30, max_steps=3, log_every_steps=1, max_grad_norm=1e30))
     with pytest.raises(FloatingPointError):
         trainer.fit()
+
+
+def test_fault_injection_fires_once_then_resume_completes(tmp_path) -> None:  # type: ignore[no-untyped-def]
+    """One simulated crash per job: the run dies at ``fail_at_step``; the restarted run resumes from
+    the last checkpoint and is not killed again (the K8s gang-restart e2e relies on this)."""
+    cfg = _cfg(max_steps=6, save_every_steps=2, extra={"fail_at_step": 5})
+    run = tmp_path / "run"
+    run.mkdir()
+    with pytest.raises(RuntimeError, match="fault injection"):
+        Trainer(cfg, run_dir=run).fit()
+    restart = tmp_path / "restart"
+    restart.mkdir()
+    result = Trainer(cfg, run_dir=restart).fit(resume_from=str(run / "checkpoints"))
+    assert result.resumed_from_step == 4 and result.final_step == 6

@@ -78,8 +78,10 @@ def make_config(args: argparse.Namespace, world: int):
         model.setdefault("extra", {})["fused"] = args.path == "fused"
     payload = {
         "schema_version": 1,
+        # deterministic=False: the fast path's split-K / embedding atomics (run.deterministic
+        # selects fixed-order reductions; synthetic data makes the data-order half moot)
         "run": {"name": f"bench-{args.model}", "seed": 1337, "device": args.device,
-                "precision": "bf16" if gpu else "fp32"},
+                "precision": "bf16" if gpu else "fp32", "deterministic": args.deterministic},
         "model": model,
         "data": {
             "name": "synthetic_tokens",
@@ -119,6 +121,7 @@ def main() -> int:
     ap.add_argument("--path", choices=["fused", "module"], default="fused")
     ap.add_argument("--dropout", type=float, default=0.0, help="model dropout (reference default 0.1)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda", help="cpu: contract tests only")
+    ap.add_argument("--deterministic", action="store_true", help="fixed-order reductions (run.deterministic)")
     args = ap.parse_args()
 
     if args.gpus < 1:
@@ -215,6 +218,7 @@ def main() -> int:
                 "path": args.path,
                 "dropout": args.dropout,
                 "grad_reduce_dtype": args.grad_reduce_dtype,
+                "deterministic": args.deterministic,
                 "backend": dist.get_backend() if world > 1 else None,
             },
             "tokens_per_sec_per_gpu": round(tps / world, 1),

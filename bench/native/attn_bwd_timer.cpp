@@ -55,11 +55,12 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
-  for (int i = 0; i < 5; ++i) CHECK(llmt::launch_attn_bwd(dout, qkv, out, lse, dqkv, delta, dq, nullptr, dims, llmt::DropoutArgs{}, 0));
+  for (int i = 0; i < 5; ++i)
+    CHECK(llmt::launch_attn_bwd(dout, qkv, out, lse, dqkv, delta, dq, nullptr, nullptr, dims, llmt::DropoutArgs{}, 0));
   std::vector<float> ms;
   for (int i = 0; i < 30; ++i) {
     CHECK(hipEventRecord(a, 0));
-    CHECK(llmt::launch_attn_bwd(dout, qkv, out, lse, dqkv, delta, dq, nullptr, dims, llmt::DropoutArgs{}, 0));
+    CHECK(llmt::launch_attn_bwd(dout, qkv, out, lse, dqkv, delta, dq, nullptr, nullptr, dims, llmt::DropoutArgs{}, 0));
     CHECK(hipEventRecord(b, 0));
     CHECK(hipEventSynchronize(b));
     float t;

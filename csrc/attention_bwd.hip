@@ -38,16 +38,19 @@ constexpr int kQTile = 64;  // query rows per sweep step (two 32-row MFMA tiles)
 
 // delta[b, h, t] = sum_d dO[b, t, h, d] * O[b, t, h, d]; a workgroup owns kDeltaRows consecutive t
 // of one (b, h) in kDeltaRows / 32 unrolled sweeps of 32 rows (8 lanes per row, every sweep's
-// loads issued up front).  With `dbias_v` it also accumulates the column sums of dO per head:
-// without dropout every valid row of P sums to 1, so sum_key dV[key, d] = sum_q dO[q, d] — the
-// V part of the qkv-bias gradient costs one LDS reduction here instead of a pass over dqkv.
-// 256 rows per workgroup keep the float atomics at 64 per 256 rows: with 32-row workgroups the
-// 64 addresses of a head took B*T/32 atomics each and the kernel ran at 1.8 TB/s.
+// loads issued up front).  With `vparts` it also forms the column sums of dO per head: without
+// dropout every valid row of P sums to 1, so sum_key dV[key, d] = sum_q dO[q, d] — the V part of
+// the qkv-bias gradient costs one LDS reduction here instead of a pass over dqkv.  Each
+// workgroup stores its hd partial sums to vparts[b * gridDim.x + blockIdx.x][h * hd + d] (no
+// atomics: 512+ workgroups per head would serialise on the same 64 addresses);
+// launch_colsum_reduce sums them in a fixed order.
 constexpr int kDeltaRows = 256;
+template <bool SMALLHD>
 __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restrict__ dout,
                                                          const bf16_raw* __restrict__ out,
-                                                         float* __restrict__ delta, float* __restrict__ dbias_v,
-                                                         int T, int H, int hd) {
+                                                         float* __restrict__ delta, float* __restrict__ vparts,
+                                                         int T, int H, int hd_arg) {
+  const int hd = SMALLHD ? hd_arg : kHD;
   __shared__ float red[4][kHD];
   const int bh = blockIdx.y;
   const int b = bh / H, h = bh - b * H;
@@ -83,7 +86,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
     const int t = blockIdx.x * kDeltaRows + 32 * it + rl;
     if (t < T && sub == 0) delta[(long)bh * T + t] = acc;
   }
-  if (dbias_v == nullptr) return;  // uniform: kernel argument
+  if (vparts == nullptr) return;  // uniform: kernel argument
   // column sums: over the wave's 8 rows with shuffles (lanes sharing `sub`), then the 4 waves
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -99,7 +102,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
   __syncthreads();
   if (threadIdx.x < hd) {
     const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    atomicAdd(dbias_v + h * hd + threadIdx.x, s);
+    vparts[((long)b * gridDim.x + blockIdx.x) * (H * hd) + h * hd + threadIdx.x] = s;
   }
 }
 
@@ -108,11 +111,14 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
 // atomics); rows only ever read the partials their causal key blocks wrote.  A workgroup owns
 // kDqRows rows t of one (b, h) inside one 256-key block, so all its rows sum the same number of
 // planes; row tiles are dispatched last-first (most planes first) and the Q part of the qkv-bias
-// gradient (column sums of dQ) leaves the workgroup as 64 atomics per kDqRows rows.
+// gradient (column sums of dQ) leaves the workgroup as one partial row,
+// qparts[b * gridDim.y + tile][h * hd + d] (fixed-order reduce afterwards, no atomics).
 constexpr int kDqRows = 64;
+template <bool SMALLHD>
 __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const float* __restrict__ part, bf16_raw* __restrict__ dqkv,
-                                                             float* __restrict__ dbias, int T, int H, int hd, int nkb,
-                                                             long plane) {
+                                                             float* __restrict__ qparts, int T, int H, int hd_arg,
+                                                             int nkb, long plane) {
+  const int hd = SMALLHD ? hd_arg : kHD;
   __shared__ float red[4][kHD];
   const int bh = blockIdx.x;
   const int b = bh / H, h = bh - b * H;
@@ -151,7 +157,7 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const float* __rest
       for (int j = 0; j < 8; ++j) csum[j] += f[it][j];
     }
   }
-  if (dbias == nullptr) return;  // uniform: kernel argument
+  if (qparts == nullptr) return;  // uniform: kernel argument
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     csum[j] += __shfl_xor(csum[j], 8, 64);
@@ -166,7 +172,7 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const float* __rest
   __syncthreads();
   if (threadIdx.x < hd) {
     const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    atomicAdd(dbias + h * hd + threadIdx.x, s);
+    qparts[((long)b * gridDim.y + tile) * (H * hd) + h * hd + threadIdx.x] = s;
   }
 }
 
@@ -190,7 +196,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta,
                                                           bf16_raw* __restrict__ dqkv,
-                                                          float* __restrict__ dq_part, float* __restrict__ dbias,
+                                                          float* __restrict__ dq_part, float* __restrict__ vparts,
                                                           int T, int H, int nkb, DropoutArgs dr, int hd_arg,
                                                           float scale_arg, const uint8_t* __restrict__ key_valid) {
   __shared__ __attribute__((aligned(16))) bf16_raw kt_lds[kHD * kKvBlk];             // K^T, 32 KB
@@ -239,13 +245,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   bf16x8 kf[4], vf[4];
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
+    // fragments past a small head dim load zeros through an out-of-record offset (a real read of
+    // the last key's last head would run past the end of the qkv allocation)
+    const bool live = !SMALLHD || 16 * kk + 8 * half < hd;
     const int off = (int)(key * row_stride + 16 * kk + 8 * half) * 2;
-    kf[kk] = __builtin_bit_cast(bf16x8, buf_load16(r_kv, off + hd * H * 2));
-    vf[kk] = __builtin_bit_cast(bf16x8, buf_load16(r_kv, off + 2 * hd * H * 2));
-    if (SMALLHD && 16 * kk + 8 * half >= hd) {
-      kf[kk] = __builtin_bit_cast(bf16x8, ushort8_t{0, 0, 0, 0, 0, 0, 0, 0});
-      vf[kk] = kf[kk];
-    }
+    kf[kk] = __builtin_bit_cast(bf16x8, buf_load16(r_kv, live ? off + hd * H * 2 : kOobOff));
+    vf[kk] = __builtin_bit_cast(bf16x8, buf_load16(r_kv, live ? off + 2 * hd * H * 2 : kOobOff));
   }
   // K^T image for dQ = dS K (B operand read 8 keys at a time); written from the K fragments
 #pragma unroll
@@ -264,9 +269,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
       const int cidx = threadIdx.x + 512 * i;
       const int r = (cidx >> 3) & 63, ch = cidx & 7;
       const int qrow = q0 + r;
-      stg[i] = i == 0 ? buf_load16(r_q, (int)(qrow * row_stride + ch * 8) * 2)
-                      : buf_load16(r_do, (int)(qrow * out_stride + ch * 8) * 2);
-      if (SMALLHD && ch * 8 >= hd) stg[i] = ushort8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      const bool live = !SMALLHD || ch * 8 < hd;
+      stg[i] = i == 0 ? buf_load16(r_q, live ? (int)(qrow * row_stride + ch * 8) * 2 : kOobOff)
+                      : buf_load16(r_do, live ? (int)(qrow * out_stride + ch * 8) * 2 : kOobOff);
     }
     if (threadIdx.x < 2 * kQTile) {
       const int qq = q0 + (threadIdx.x & (kQTile - 1));
@@ -460,8 +465,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   // qkv-bias gradient, K and V parts.  K: exactly zero — adding b_k shifts every score of a query
   // row by q.b_k, which softmax ignores — so nothing is accumulated.  V without dropout: the
   // delta kernel's column sums of dO.  V with dropout (rows of the dropped P no longer sum to 1):
-  // sum this block's 256 keys of dV^T — over the 32 lanes of each half, then over the 8 waves.
-  if (!DROPOUT || dbias == nullptr) return;
+  // sum this block's 256 keys of dV^T — over the 32 lanes of each half, then over the 8 waves —
+  // into this block's partial row vparts[b * nkb + kb][h * hd + d].
+  if (!DROPOUT || vparts == nullptr) return;
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt) {
 #pragma unroll
@@ -477,7 +483,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
     float acc = 0.f;
 #pragma unroll
     for (int w = 0; w < kBwdWaves; ++w) acc += bias_red[w][threadIdx.x];
-    atomicAdd(dbias + (2 * H + h) * hd + threadIdx.x, acc);
+    vparts[((long)b * nkb + kb) * (H * hd) + h * hd + threadIdx.x] = acc;
   }
 }
 
@@ -488,43 +494,83 @@ long attn_bwd_workspace_floats(int B, int T, int H) {
   return nkb * B * H * (long)T * attn::kHD;
 }
 
+namespace {
+// partial rows of the qkv-bias column sums: V (delta kernel or, with dropout, the main kernel)
+// and Q (dQ reduce), then the fixed-order reduce's scratch
+struct BiasParts {
+  int nv, nq;
+  long cols;
+};
+BiasParts bias_parts(int B, int T, int H, int hd) {
+  const int nkb = (T + attn::kKvBlk - 1) / attn::kKvBlk;
+  const int nv1 = B * ((T + attn::kDeltaRows - 1) / attn::kDeltaRows), nv2 = B * nkb;
+  return {nv1 > nv2 ? nv1 : nv2, B * ((T + attn::kDqRows - 1) / attn::kDqRows), (long)H * hd};
+}
+}  // namespace
+
+long attn_bwd_bias_ws_floats(int B, int T, int H, int hd) {
+  const BiasParts p = bias_parts(B, T, H, hd);
+  const long sv = colsum_scratch_floats(p.nv, p.cols), sq = colsum_scratch_floats(p.nq, p.cols);
+  return (long)(p.nv + p.nq) * p.cols + (sv > sq ? sv : sq);
+}
+
 template <bool DROPOUT, bool KMASK, bool SMALLHD>
 static void launch_bwd_variant(dim3 grid, hipStream_t stream, const bf16_raw* qkv, const bf16_raw* dout,
-                               const float* lse, const float* delta, bf16_raw* dqkv, float* dq_part, float* dbias,
+                               const float* lse, const float* delta, bf16_raw* dqkv, float* dq_part, float* vparts,
                                const AttnDims& d, int nkb, DropoutArgs dr) {
   hipLaunchKernelGGL((attn::attn_bwd_kernel<DROPOUT, KMASK, SMALLHD>), grid, dim3(512), 0, stream, qkv, dout, lse,
-                     delta, dqkv, dq_part, dbias, d.T, d.H, nkb, dr, d.hd, d.scale, d.key_valid);
+                     delta, dqkv, dq_part, vparts, d.T, d.H, nkb, dr, d.hd, d.scale, d.key_valid);
 }
 
 hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse, void* dqkv,
-                           float* delta, float* dq_part, float* dbias, const AttnDims& d, DropoutArgs dropout,
-                           hipStream_t stream, bool delta_ready) {
+                           float* delta, float* dq_part, float* dbias, float* bias_ws, const AttnDims& d,
+                           DropoutArgs dropout, hipStream_t stream, bool delta_ready) {
   const int B = d.B, T = d.T, H = d.H, hd = d.hd;
   if (B <= 0 || T <= 0 || H <= 0 || T > 65535 || hd <= 0 || hd > attn::kHD || hd % 8 != 0) return hipErrorInvalidValue;
+  if (dbias != nullptr && bias_ws == nullptr) return hipErrorInvalidValue;
   const long rows = (long)B * T * H;
+  const BiasParts bp = bias_parts(B, T, H, hd);
+  float* vparts = dbias != nullptr ? bias_ws : nullptr;
+  float* qparts = dbias != nullptr ? bias_ws + (long)bp.nv * bp.cols : nullptr;
+  float* scratch = dbias != nullptr ? bias_ws + (long)(bp.nv + bp.nq) * bp.cols : nullptr;
+  const bool v_from_delta = !delta_ready && dropout.thr == 0 && dbias != nullptr;
+  const dim3 dgrid((T + attn::kDeltaRows - 1) / attn::kDeltaRows, B * H);
+  const bool small = hd != attn::kHD;
   if (!delta_ready)
-    hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((T + attn::kDeltaRows - 1) / attn::kDeltaRows, B * H), dim3(256), 0, stream,
-                       (const bf16_raw*)dout, (const bf16_raw*)out, delta,
-                       dropout.thr == 0 && dbias != nullptr ? dbias + 2L * H * hd : nullptr, T, H, hd);
+    hipLaunchKernelGGL(small ? attn::attn_delta_kernel<true> : attn::attn_delta_kernel<false>, dgrid, dim3(256), 0, stream,
+                       (const bf16_raw*)dout, (const bf16_raw*)out, delta, v_from_delta ? vparts : nullptr, T, H, hd);
   const int nkb = (T + attn::kKvBlk - 1) / attn::kKvBlk;
   const dim3 grid(B * H, nkb);
-  const bool drop = dropout.thr != 0, km = d.key_valid != nullptr, small = hd != attn::kHD;
+  const bool drop = dropout.thr != 0, km = d.key_valid != nullptr;
   const int variant = (drop ? 4 : 0) | (km ? 2 : 0) | (small ? 1 : 0);
   auto q = (const bf16_raw*)qkv;
   auto g = (const bf16_raw*)dout;
   auto dq = (bf16_raw*)dqkv;
+  float* vp = drop ? vparts : nullptr;  // the main kernel forms the V-bias partials only with dropout
   switch (variant) {
-    case 0: launch_bwd_variant<false, false, false>(grid, stream, q, g, lse, delta, dq, dq_part, dbias, d, nkb, dropout); break;
-    case 1: launch_bwd_variant<false, false, true>(grid, stream, q, g, lse, delta, dq, dq_part, dbias, d, nkb, dropout); break;
-    case 2: launch_bwd_variant<false, true, false>(grid, stream, q, g, lse, delta, dq, dq_part, dbias, d, nkb, dropout); break;
-    case 3: launch_bwd_variant<false, true, true>(grid, stream, q, g, lse, delta, dq, dq_part, dbias, d, nkb, dropout); break;
-    case 4: launch_bwd_variant<true, false, false>(grid, stream, q, g, lse, delta, dq, dq_part, dbias, d, nkb, dropout); break;
-    case 5: launch_bwd_variant<true, false, true>(grid, stream, q, g, lse, delta, dq, dq_part, dbias, d, nkb, dropout); break;
-    case 6: launch_bwd_variant<true, true, false>(grid, stream, q, g, lse, delta, dq, dq_part, dbias, d, nkb, dropout); break;
-    default: launch_bwd_variant<true, true, true>(grid, stream, q, g, lse, delta, dq, dq_part, dbias, d, nkb, dropout); break;
+    case 0: launch_bwd_variant<false, false, false>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
+    case 1: launch_bwd_variant<false, false, true>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
+    case 2: launch_bwd_variant<false, true, false>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
+    case 3: launch_bwd_variant<false, true, true>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
+    case 4: launch_bwd_variant<true, false, false>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
+    case 5: launch_bwd_variant<true, false, true>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
+    case 6: launch_bwd_variant<true, true, false>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
+    default: launch_bwd_variant<true, true, true>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
   }
-  hipLaunchKernelGGL(attn::attn_dq_reduce_kernel, dim3(B * H, (T + attn::kDqRows - 1) / attn::kDqRows), dim3(256), 0,
-                     stream, dq_part, dq, dbias, T, H, hd, nkb, rows * (long)attn::kHD);
+  const dim3 rgrid(B * H, (T + attn::kDqRows - 1) / attn::kDqRows);
+  hipLaunchKernelGGL(small ? attn::attn_dq_reduce_kernel<true> : attn::attn_dq_reduce_kernel<false>, rgrid, dim3(256),
+                     0, stream, dq_part, dq, qparts, T, H, hd, nkb, rows * (long)attn::kHD);
+  if (dbias != nullptr) {
+    // fixed-order sums of the partial rows: Q part, then (unless the out-proj GEMM's epilogue
+    // already added it) the V part; the K part of the qkv-bias gradient is exactly zero
+    hipError_t e = launch_colsum_reduce(qparts, bp.nq, bp.cols, dbias, scratch, stream);
+    if (e != hipSuccess) return e;
+    const int nv = drop ? B * nkb : (v_from_delta ? (int)dgrid.x * B : 0);
+    if (nv > 0) {
+      e = launch_colsum_reduce(vparts, nv, bp.cols, dbias + 2L * H * hd, scratch, stream);
+      if (e != hipSuccess) return e;
+    }
+  }
   return hipGetLastError();
 }
 

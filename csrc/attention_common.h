@@ -8,6 +8,9 @@ namespace llmt {
 namespace attn {
 
 constexpr int kHD = 64;  // head dim: one 128-byte bf16 row per key/query
+// a buffer-load byte offset past every descriptor's record count (records stay < 2 GiB - 64):
+// the load returns zeros without touching memory
+constexpr int kOobOff = 0x7ffffff0;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short short4v __attribute__((ext_vector_type(4)));

@@ -86,14 +86,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
     for (int i = 0; i < 2; ++i) {
       const int c = threadIdx.x + 256 * i;
       const int r = c >> 3, ch = c & 7;
-      const int off = (int)(((long)(tile * kKBlk + r) * row_stride + ch * 8 + hd * H) * 2);
-      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      // chunks past a small head dim are never read: an offset past the descriptor's record
+      // count loads zeros (reading them would run past the last head of the last token, i.e.
+      // past the end of the qkv allocation, by (64 - hd) * 2 bytes)
+      const bool live = !SMALLHD || ch * 8 < hd;
+      const int off = live ? (int)(((long)(tile * kKBlk + r) * row_stride + ch * 8 + hd * H) * 2) : kOobOff;
+      const int off_v = live ? off + hd * H * 2 : kOobOff;
       st[i] = __builtin_bit_cast(ushort8_t, __builtin_amdgcn_raw_buffer_load_b128(rkv, off, 0, 0));
-      st[2 + i] = __builtin_bit_cast(ushort8_t, __builtin_amdgcn_raw_buffer_load_b128(rkv, off + hd * H * 2, 0, 0));
-      if (SMALLHD && ch * 8 >= hd) {  // the next head's columns: zero-fill the missing dims
-        st[i] = ushort8_t{0, 0, 0, 0, 0, 0, 0, 0};
-        st[2 + i] = st[i];
-      }
+      st[2 + i] = __builtin_bit_cast(ushort8_t, __builtin_amdgcn_raw_buffer_load_b128(rkv, off_v, 0, 0));
     }
   };
   auto store_tile = [&](const ushort8_t(&st)[4], int buf) {

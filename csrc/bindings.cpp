@@ -24,6 +24,11 @@ void check_hip(hipError_t e, const char* what) {
   TORCH_CHECK(e == hipSuccess, "llmtrain_hip: ", what, " failed: ", hipGetErrorString(e));
 }
 
+// fp32 scratch from the caching allocator (stream-ordered reuse; graph-capture safe)
+Tensor workspace(const Tensor& like, long floats) {
+  return at::empty({floats > 0 ? floats : 1}, like.options().dtype(at::kFloat));
+}
+
 void check_gpu(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), "llmtrain_hip: ", name, " must be a GPU tensor");
   TORCH_CHECK(t.is_contiguous(), "llmtrain_hip: ", name, " must be contiguous");
@@ -154,7 +159,11 @@ std::tuple<Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor& xs, con
   a.M = (int)M;
   a.d = (int)d;
   a.dropout = make_dropout(dropout_p, dropout_seed);
-  if (M > 0) check_hip(llmt::launch_layernorm_bwd(a, cur_stream()), "layernorm_bwd");
+  if (M > 0) {
+    Tensor ws = workspace(xs, llmt::layernorm_bwd_ws_floats(a));
+    a.ws = ws.data_ptr<float>();
+    check_hip(llmt::launch_layernorm_bwd(a, cur_stream()), "layernorm_bwd");
+  }
   return {dx, dx_lp};
 }
 
@@ -220,10 +229,12 @@ Tensor gelu_bwd(const Tensor& dg, const Tensor& u, const c10::optional<Tensor>& 
   }
   at::hip::HIPGuardMasqueradingAsCUDA guard(u.device());
   Tensor du = at::empty_like(u);
-  if (M > 0)
-    check_hip(llmt::launch_gelu_bwd(dg.data_ptr(), u.data_ptr(), du.data_ptr(), db, is_lowp(u, "u"), (int)M, (int)F,
-                                    cur_stream()),
+  if (M > 0) {
+    Tensor ws = workspace(u, db != nullptr ? llmt::colwise_ws_floats((int)M, (int)F) : 0);
+    check_hip(llmt::launch_gelu_bwd(dg.data_ptr(), u.data_ptr(), du.data_ptr(), db, ws.data_ptr<float>(),
+                                    is_lowp(u, "u"), (int)M, (int)F, cur_stream()),
               "gelu_bwd");
+  }
   return du;
 }
 
@@ -234,10 +245,12 @@ void colsum_accum(const Tensor& dy, Tensor out) {
   TORCH_CHECK(dy.dim() == 2 && out.numel() == dy.size(1), "dy [M, N], out [N]");
   TORCH_CHECK(dy.size(1) % 8 == 0, "colsum needs N % 8 == 0");
   at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
-  if (dy.size(0) > 0)
-    check_hip(llmt::launch_colsum_accum(dy.data_ptr(), is_lowp(dy, "dy"), out.data_ptr<float>(), (int)dy.size(0),
-                                        (int)dy.size(1), cur_stream()),
+  if (dy.size(0) > 0) {
+    Tensor ws = workspace(out, llmt::colwise_ws_floats((int)dy.size(0), (int)dy.size(1)));
+    check_hip(llmt::launch_colsum_accum(dy.data_ptr(), is_lowp(dy, "dy"), out.data_ptr<float>(), ws.data_ptr<float>(),
+                                        (int)dy.size(0), (int)dy.size(1), cur_stream()),
               "colsum_accum");
+  }
 }
 
 Tensor embedding_fwd(const Tensor& ids, const Tensor& wte, const Tensor& wpe, double dropout_p, int64_t dropout_seed) {
@@ -273,11 +286,24 @@ void embedding_bwd(const Tensor& dx, const Tensor& ids, Tensor dwte, Tensor dwpe
   const int64_t B = ids.size(0), T = ids.size(1), d = dwte.size(1);
   TORCH_CHECK(dx.size(0) == B * T && dx.size(1) == d && dwpe.size(0) >= T && dwpe.size(1) == d, "embedding shapes");
   at::hip::HIPGuardMasqueradingAsCUDA guard(dx.device());
-  if (B * T > 0)
-    check_hip(llmt::launch_embedding_bwd(dx.data_ptr<float>(), ids.data_ptr<int64_t>(), dwte.data_ptr<float>(),
-                                         dwpe.data_ptr<float>(), (int)B, (int)T, (int)d, (int)dwte.size(0),
-                                         make_dropout(dropout_p, dropout_seed), cur_stream()),
-              "embedding_bwd");
+  if (B * T == 0) return;
+  const llmt::DropoutArgs dr = make_dropout(dropout_p, dropout_seed);
+  check_hip(llmt::launch_embedding_bwd(dx.data_ptr<float>(), ids.data_ptr<int64_t>(),
+                                       llmt::deterministic() ? nullptr : dwte.data_ptr<float>(),
+                                       dwpe.data_ptr<float>(), (int)B, (int)T, (int)d, (int)dwte.size(0), dr,
+                                       cur_stream()),
+            "embedding_bwd");
+  if (llmt::deterministic()) {
+    // token gradient in a fixed order: stable sort of the token ids (rocPRIM radix sort), then one
+    // wave per run of equal tokens sums its dx rows in sorted order (no atomics)
+    auto sorted = ids.reshape({-1}).sort(/*stable=*/true, /*dim=*/0, /*descending=*/false);
+    const Tensor& sorted_ids = std::get<0>(sorted);
+    const Tensor& order = std::get<1>(sorted);
+    check_hip(llmt::launch_embedding_bwd_sorted(dx.data_ptr<float>(), sorted_ids.data_ptr<int64_t>(),
+                                                order.data_ptr<int64_t>(), dwte.data_ptr<float>(), (int)(B * T),
+                                                (int)d, (int)dwte.size(0), dr, cur_stream()),
+              "embedding_bwd_sorted");
+  }
 }
 
 // ---- attention -------------------------------------------------------------------------------
@@ -355,6 +381,7 @@ Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const 
     delta = at::empty({B, H, T}, lse.options());
   }
   Tensor dq = at::empty({llmt::attn_bwd_workspace_floats((int)B, (int)T, (int)H)}, lse.options());
+  Tensor bias_ws = workspace(lse, dbias.has_value() ? llmt::attn_bwd_bias_ws_floats((int)B, (int)T, (int)H, (int)hd) : 0);
   float* db = nullptr;
   if (dbias.has_value()) {
     check_gpu(*dbias, "dbias");
@@ -363,11 +390,16 @@ Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const 
     db = dbias->data_ptr<float>();
   }
   check_hip(llmt::launch_attn_bwd(dout.data_ptr(), qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
-                                  dqkv.data_ptr(), delta.data_ptr<float>(), dq.data_ptr<float>(), db, dims,
+                                  dqkv.data_ptr(), delta.data_ptr<float>(), dq.data_ptr<float>(), db,
+                                  bias_ws.data_ptr<float>(), dims,
                                   make_dropout(dropout_p, dropout_seed), cur_stream(), delta_in.has_value()),
             "attn_bwd");
   return dqkv;
 }
+
+// process-wide deterministic mode (run.deterministic): fixed-order split-K / embedding reductions
+void set_deterministic(bool on) { llmt::set_deterministic(on); }
+bool get_deterministic() { return llmt::deterministic(); }
 
 // keep-mask of `n` consecutive elements of one dropout site (tests / debugging)
 Tensor dropout_mask(int64_t n, double p, int64_t seed, const Tensor& like) {
@@ -390,9 +422,13 @@ void wgrad_gemm(const Tensor& dy, const Tensor& x, Tensor c, int64_t split, int6
   const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
   TORCH_CHECK(x.size(0) == M && c.size(0) == N && c.size(1) == K, "wgrad_gemm: shape mismatch");
   at::hip::HIPGuardMasqueradingAsCUDA guard(c.device());
+  // deterministic mode: per-M-chunk partial slabs, reduced in a fixed order (no split-K atomics)
+  const long det = llmt::wgrad_gemm_det_ws_floats((int)dy.stride(0), (int)x.stride(0), (int)M, (int)N, (int)K,
+                                                  (int)split, (int)tile);
+  Tensor ws = workspace(c, det);
   check_hip(llmt::launch_wgrad_gemm(dy.data_ptr(), (int)dy.stride(0), x.data_ptr(), (int)x.stride(0),
                                     c.data_ptr<float>(), (int)c.stride(0), (int)M, (int)N, (int)K, (int)split,
-                                    (int)tile, cur_stream()),
+                                    (int)tile, cur_stream(), det > 0 ? ws.data_ptr<float>() : nullptr),
             "wgrad_gemm");
 }
 
@@ -462,6 +498,8 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tens
       g.dbias = dbias->data_ptr<float>();
     }
   }
+  Tensor ws = workspace(a, g.dbias != nullptr ? llmt::gemm_fused_ws_floats((int)M, (int)N) : 0);
+  g.ws = ws.data_ptr<float>();
   if (M > 0) check_hip(llmt::launch_gemm_fused(g, cur_stream()), "gemm_fused");
   return {out, out2};
 }
@@ -538,6 +576,8 @@ TORCH_LIBRARY(llmtrain_hip, m) {
   m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, int B, int T, int H, float dropout_p=0.,"
         " int dropout_seed=0, Tensor(a!)? dbias=None, Tensor? delta=None, Tensor? key_valid=None) -> Tensor");
   m.def("dropout_mask(int n, float p, int seed, Tensor like) -> Tensor");
+  m.def("set_deterministic(bool on) -> ()", &set_deterministic);  // catch-all: no tensor arguments
+  m.def("get_deterministic() -> bool", &get_deterministic);
   m.def("wgrad_gemm(Tensor dy, Tensor x, Tensor(a!) c, int split=0, int tile=0) -> ()");
   m.def("gemm_fused(Tensor a, Tensor b, bool b_kn, int epilogue, Tensor? bias=None, Tensor? u=None,"
         " Tensor(a!)? dbias=None, int seq_len=0) -> (Tensor, Tensor?)");

@@ -142,9 +142,11 @@ __global__ __launch_bounds__(256) void colwise_kernel(const void* __restrict__ a
 #pragma unroll
   for (int k = 0; k < 8; ++k) part[wid][lane * 8 + k] = acc[k];
   __syncthreads();
+  // this row block's partial column sums (one row of `colsum` = [gridDim.y][F8 * 8] partials,
+  // summed in a fixed order by launch_colsum_reduce: no atomics)
   for (int i = threadIdx.x; i < 64 * 8; i += 256) {
     const int col = blockIdx.x * 512 + i;
-    if (col < F8 * 8) atomicAdd(colsum + col, part[0][i] + part[1][i] + part[2][i] + part[3][i]);
+    if (col < F8 * 8) colsum[(long)blockIdx.y * F8 * 8 + col] = part[0][i] + part[1][i] + part[2][i] + part[3][i];
   }
 }
 
@@ -249,27 +251,34 @@ hipError_t launch_scale(const void* x, void* y, const float* scale, bool bf16, l
   return hipGetLastError();
 }
 
-hipError_t launch_gelu_bwd(const void* dg, const void* u, void* du, float* dbias, bool bf16, int M,
+long colwise_ws_floats(int M, int N) {
+  const int rpb = rows_per_block_for(M), nparts = (M + rpb - 1) / rpb;
+  return (long)nparts * N + colsum_scratch_floats(nparts, N);
+}
+
+hipError_t launch_gelu_bwd(const void* dg, const void* u, void* du, float* dbias, float* ws, bool bf16, int M,
                            int F, hipStream_t stream) {
-  if (F % 8 != 0) return hipErrorInvalidValue;
+  if (F % 8 != 0 || (dbias != nullptr && ws == nullptr)) return hipErrorInvalidValue;
   const int F8 = F / 8, rpb = rows_per_block_for(M);
   dim3 grid((F8 + 63) / 64, (M + rpb - 1) / rpb);
+  float* parts = dbias != nullptr ? ws : nullptr;
   if (bf16)
-    hipLaunchKernelGGL((colwise_kernel<0, true>), grid, dim3(256), 0, stream, dg, u, du, dbias, M, F8, rpb);
+    hipLaunchKernelGGL((colwise_kernel<0, true>), grid, dim3(256), 0, stream, dg, u, du, parts, M, F8, rpb);
   else
-    hipLaunchKernelGGL((colwise_kernel<0, false>), grid, dim3(256), 0, stream, dg, u, du, dbias, M, F8, rpb);
+    hipLaunchKernelGGL((colwise_kernel<0, false>), grid, dim3(256), 0, stream, dg, u, du, parts, M, F8, rpb);
+  if (dbias != nullptr) return launch_colsum_reduce(parts, (int)grid.y, F, dbias, ws + (long)grid.y * F, stream);
   return hipGetLastError();
 }
 
-hipError_t launch_colsum_accum(const void* dy, bool bf16, float* out, int M, int N, hipStream_t stream) {
-  if (N % 8 != 0) return hipErrorInvalidValue;
+hipError_t launch_colsum_accum(const void* dy, bool bf16, float* out, float* ws, int M, int N, hipStream_t stream) {
+  if (N % 8 != 0 || ws == nullptr) return hipErrorInvalidValue;
   const int N8 = N / 8, rpb = rows_per_block_for(M);
   dim3 grid((N8 + 63) / 64, (M + rpb - 1) / rpb);
   if (bf16)
-    hipLaunchKernelGGL((colwise_kernel<1, true>), grid, dim3(256), 0, stream, dy, nullptr, nullptr, out, M, N8, rpb);
+    hipLaunchKernelGGL((colwise_kernel<1, true>), grid, dim3(256), 0, stream, dy, nullptr, nullptr, ws, M, N8, rpb);
   else
-    hipLaunchKernelGGL((colwise_kernel<1, false>), grid, dim3(256), 0, stream, dy, nullptr, nullptr, out, M, N8, rpb);
-  return hipGetLastError();
+    hipLaunchKernelGGL((colwise_kernel<1, false>), grid, dim3(256), 0, stream, dy, nullptr, nullptr, ws, M, N8, rpb);
+  return launch_colsum_reduce(ws, (int)grid.y, N, out, ws + (long)grid.y * N, stream);
 }
 
 hipError_t launch_embedding_fwd(const int64_t* ids, const float* wte, const float* wpe, float* x, int B,
@@ -285,8 +294,9 @@ hipError_t launch_embedding_bwd(const float* dx, const int64_t* ids, float* dwte
                                 int d, int V, DropoutArgs dropout, hipStream_t stream) {
   if (d % 4 != 0) return hipErrorInvalidValue;
   const int M = B * T;
-  hipLaunchKernelGGL(embedding_bwd_tok_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, dx, ids, dwte, M, d, V,
-                     dropout);
+  if (dwte != nullptr)  // nullptr: the caller scatters the token gradient itself (deterministic mode)
+    hipLaunchKernelGGL(embedding_bwd_tok_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, dx, ids, dwte, M, d, V,
+                       dropout);
   const long work = (long)T * (d / 4);
   hipLaunchKernelGGL(embedding_bwd_pos_kernel, dim3((work + 255) / 256), dim3(256), 0, stream, dx, dwpe, B, T, d,
                      dropout);

@@ -191,7 +191,7 @@ struct Args {
   bf16_raw* C2;          // EPI 1: gelu output
   const bf16_raw* bias;  // EPI 0/1 (optional for 0)
   const bf16_raw* U;     // EPI 2: pre-activation; EPI 3: attention output O
-  float* dbias;          // EPI 2/3: column sums (optional)
+  float* dbias;          // EPI 2/3: column sums (optional) -> partial rows [ceil(M / 128)][N] (see below)
   float* delta;          // EPI 3: [M / T, N / 64, T] per-head row dot products
   int T;                 // EPI 3: rows per sequence
   int lda, ldb, ldc, ldu;
@@ -504,9 +504,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
         v += __shfl_xor(v, 32, 64);
         csum[k] = v;
       }
+      // this wave's 128-row block owns partial row mw / 128 of the column sums (plain stores; the
+      // launcher's fixed-order reduce adds the rows to the bias gradient: no atomics)
       if (lane < 8 && n < p.N) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) atomicAdd(p.dbias + n + k, csum[k]);
+        float* dst = p.dbias + (long)(mw / 128) * p.N + n;
+        *reinterpret_cast<float4_t*>(dst) = float4_t{csum[0], csum[1], csum[2], csum[3]};
+        *reinterpret_cast<float4_t*>(dst + 4) = float4_t{csum[4], csum[5], csum[6], csum[7]};
       }
     }
   }
@@ -541,7 +544,9 @@ hipError_t launch_gemm_fused(const GemmFusedArgs& g, hipStream_t stream) {
   a.C2 = (bf16_raw*)g.c2;
   a.bias = (const bf16_raw*)g.bias;
   a.U = (const bf16_raw*)g.u;
-  a.dbias = g.dbias;
+  const int nparts = (g.M + 127) / 128;
+  if (g.dbias != nullptr && g.ws == nullptr) return hipErrorInvalidValue;
+  a.dbias = g.dbias != nullptr ? g.ws : nullptr;
   a.delta = g.delta;
   a.T = g.T;
   a.lda = g.lda;
@@ -583,6 +588,7 @@ hipError_t launch_gemm_fused(const GemmFusedArgs& g, hipStream_t stream) {
     case 6: launch_one<false, 3>(a, stream); break;
     default: launch_one<true, 3>(a, stream); break;
   }
+  if (g.dbias != nullptr) return launch_colsum_reduce(g.ws, nparts, g.N, g.dbias, g.ws + (long)nparts * g.N, stream);
   return hipGetLastError();
 }
 

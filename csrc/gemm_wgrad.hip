@@ -36,7 +36,10 @@
 //    lane-linear), which puts the 4 rows of each transposed read on distinct 64-byte bank groups;
 //  * work items are remapped so the workgroups of one M chunk run on one XCD and share its L2;
 //  * epilogue: one f32 atomic per accumulator register and lane — lanes 0-31 / 32-63 each add a
-//    contiguous 128-byte row segment, the full-rate atomic shape.
+//    contiguous 128-byte row segment, the full-rate atomic shape;
+//  * deterministic mode (run.deterministic): the same stores go to this M chunk's own partial
+//    slab [chunk][N][K] instead, and launch_colsum_reduce adds the slabs to C in chunk order —
+//    bitwise reproducible at the cost of one extra pass over split x N x K floats.
 #include <cstdlib>
 
 #include "common.h"
@@ -66,7 +69,7 @@ struct Cfg {
 template <int TN, int TK>
 __global__ __launch_bounds__(kThreads, (Cfg<TN, TK>::kMinBlocks)) void wgrad_kernel(
     const bf16_raw* __restrict__ A, int lda, const bf16_raw* __restrict__ B, int ldb, float* __restrict__ C,
-    int ldc, int M, int N, int K, int tiles, int tiles_k, int m_chunk, int nwg) {
+    int ldc, int M, int N, int K, int tiles, int tiles_k, int m_chunk, int nwg, float* __restrict__ slabs) {
   using G = Cfg<TN, TK>;
   __shared__ __attribute__((aligned(16))) bf16_raw smem[NSLOT * G::kSlotElems];
   const int lane = threadIdx.x & 63;
@@ -157,7 +160,9 @@ __global__ __launch_bounds__(kThreads, (Cfg<TN, TK>::kMinBlocks)) void wgrad_ker
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
         const int n = n0 + wn * 32 * TN + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * half;
-        if (n < N) atomicAdd(C + (long)n * ldc + k, acc[i][j][rr]);
+        if (n >= N) continue;
+        if (slabs != nullptr) slabs[((long)chunk * N + n) * K + k] = acc[i][j][rr];
+        else atomicAdd(C + (long)n * ldc + k, acc[i][j][rr]);
       }
     }
   }
@@ -170,7 +175,7 @@ struct Plan {
 
 // Modelled time of one configuration: rounds of workgroups x per-workgroup MFMA time at the
 // tile's measured efficiency, plus the split-K atomic traffic at the chip-wide atomic rate.
-Plan plan_for(int tile, int M, int N, int K, int split_req, int ncu, int min_split) {
+Plan plan_for(int tile, int M, int N, int K, int split_req, int ncu, int min_split, bool det) {
   Plan p;
   p.tile = tile;
   const int bn = tile, bk = tile;
@@ -189,7 +194,8 @@ Plan plan_for(int tile, int M, int N, int K, int split_req, int ncu, int min_spl
     const long long nwg = (long long)p.tiles * ss;
     const long long rounds = (nwg + slots - 1) / slots;
     const double t_wg = 2.0 * chunk * bn * bk / rate_cu;
-    const double t_atomic = (double)nwg * bn * bk * 4.0 / 1.3e12;
+    // atomics at ~1.3 TB/s chip-wide; deterministic slabs: stored once and read once at ~5 TB/s
+    const double t_atomic = det ? (double)nwg * bn * bk * 8.0 / 5e12 : (double)nwg * bn * bk * 4.0 / 1.3e12;
     const double cost = rounds * t_wg + t_atomic;
     if (cost < out.cost) {
       out.cost = cost;
@@ -209,11 +215,9 @@ Plan plan_for(int tile, int M, int N, int K, int split_req, int ncu, int min_spl
 
 }  // namespace wgrad
 
-hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N,
-                             int K, int split, int tile, hipStream_t stream) {
-  if (M <= 0 || N <= 0 || K <= 0) return hipSuccess;
-  // N needs no alignment: tiles past N read the next rows' data (or zeros past the chunk) into
-  // accumulators whose atomics the epilogue masks with n < N (the LM head's N = 50257)
+namespace {
+// the launcher's plan (split, tile): shared by the launch and the deterministic workspace query
+hipError_t plan_wgrad(int lda, int ldb, int M, int N, int K, int split, int tile, wgrad::Plan& p) {
   if (lda % 8 || ldb % 8 || K % 8 || lda < N) return hipErrorInvalidValue;
   if (tile == 0) {
     static const int forced = [] {
@@ -232,27 +236,53 @@ hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, fl
   // 32-bit buffer offsets: one M chunk of either operand must stay below 2 GiB (wide rows such
   // as the LM head's 50304-column logits force a minimum split)
   const long long row_bytes = 2LL * (lda > ldb ? lda : ldb);
-  const int min_split = (int)(((long long)M * row_bytes + (1LL << 31) - 1 - 4096) / ((1LL << 31) - 4096 - row_bytes * 32));
-  wgrad::Plan p;
+  const int min_split =
+      (int)(((long long)M * row_bytes + (1LL << 31) - 1 - 4096) / ((1LL << 31) - 4096 - row_bytes * 32));
+  const int ms = min_split > 0 ? min_split : 1;
+  const bool det = deterministic();
   if (tile == 128 || tile == 256) {
-    p = wgrad::plan_for(tile, M, N, K, split, ncu, min_split > 0 ? min_split : 1);
+    p = wgrad::plan_for(tile, M, N, K, split, ncu, ms, det);
   } else {
-    const wgrad::Plan a = wgrad::plan_for(256, M, N, K, split, ncu, min_split > 0 ? min_split : 1);
-    const wgrad::Plan b = wgrad::plan_for(128, M, N, K, split, ncu, min_split > 0 ? min_split : 1);
+    const wgrad::Plan a = wgrad::plan_for(256, M, N, K, split, ncu, ms, det);
+    const wgrad::Plan b = wgrad::plan_for(128, M, N, K, split, ncu, ms, det);
     p = a.cost <= b.cost ? a : b;
   }
   // 32-bit buffer offsets: one chunk of either operand must stay below 2 GiB
   if ((long long)p.m_chunk * (lda > ldb ? lda : ldb) * 2 >= (1LL << 31)) return hipErrorInvalidValue;
+  return hipSuccess;
+}
+}  // namespace
+
+long wgrad_gemm_det_ws_floats(int lda, int ldb, int M, int N, int K, int split, int tile) {
+  if (M <= 0 || N <= 0 || K <= 0 || !deterministic()) return 0;
+  wgrad::Plan p;
+  if (plan_wgrad(lda, ldb, M, N, K, split, tile, p) != hipSuccess) return 0;
+  return (long)p.split * N * K + colsum_scratch_floats(p.split, (long)N * K);
+}
+
+hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N,
+                             int K, int split, int tile, hipStream_t stream, float* det_ws) {
+  if (M <= 0 || N <= 0 || K <= 0) return hipSuccess;
+  // N needs no alignment: tiles past N read the next rows' data (or zeros past the chunk) into
+  // accumulators whose stores the epilogue masks with n < N (the LM head's N = 50257)
+  wgrad::Plan p;
+  const hipError_t e = plan_wgrad(lda, ldb, M, N, K, split, tile, p);
+  if (e != hipSuccess) return e;
+  const bool det = deterministic();
+  if (det && det_ws == nullptr) return hipErrorInvalidValue;
+  float* slabs = det ? det_ws : nullptr;
   const int nwg = p.tiles * p.split;
   if (p.tile == 256) {
     hipLaunchKernelGGL((wgrad::wgrad_kernel<4, 4>), dim3(nwg), dim3(wgrad::kThreads), 0, stream,
                        (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k,
-                       p.m_chunk, nwg);
+                       p.m_chunk, nwg, slabs);
   } else {
     hipLaunchKernelGGL((wgrad::wgrad_kernel<2, 2>), dim3(nwg), dim3(wgrad::kThreads), 0, stream,
                        (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k,
-                       p.m_chunk, nwg);
+                       p.m_chunk, nwg, slabs);
   }
+  if (det)  // slabs of chunks that had no rows (split > M / BM) were never written: only p.split exist
+    return launch_colsum_reduce(slabs, p.split, (long)N * K, c, slabs + (long)p.split * N * K, stream, K, ldc);
   return hipGetLastError();
 }
 

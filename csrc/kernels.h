@@ -53,7 +53,11 @@ struct LnBwdArgs {
   float* dproj;          // optional [d] accumulated column sum of dx
   int M, d;
   DropoutArgs dropout;   // mask of the branch that fed this stream: applied to dx_lp and dproj
+  float* ws;             // layernorm_bwd_ws_floats(*this) floats: partial rows of dw / db / dproj
 };
+// dw, db, dproj are reduced over rows through per-workgroup partial rows in `ws` and a fixed-order
+// reduce (no atomics); the workspace size depends on M, d, the dtypes and whether dproj is set
+long layernorm_bwd_ws_floats(const LnBwdArgs& a);
 hipError_t launch_layernorm_bwd(const LnBwdArgs& a, hipStream_t stream);
 
 // ---- softmax cross-entropy (forward + in-place gradient) --------------------------------
@@ -67,11 +71,14 @@ hipError_t launch_cross_entropy_fwd_bwd(void* logits, bool bf16, const int64_t* 
 // y = x * scale[0] (device scalar), fp32 math, bf16 or fp32 storage; n % 8 == 0
 hipError_t launch_scale(const void* x, void* y, const float* scale, bool bf16, long long n, hipStream_t stream);
 hipError_t launch_gelu_fwd(const void* u, void* g, bool bf16, long long n, hipStream_t stream);
-// du = dg * gelu'(u); dbias (optional, [F]) += colsum(du); tensors are [M, F]
-hipError_t launch_gelu_bwd(const void* dg, const void* u, void* du, float* dbias, bool bf16,
+// du = dg * gelu'(u); dbias (optional, [F]) += colsum(du); tensors are [M, F].  The column sums go
+// through partial rows in `ws` (colwise_ws_floats(M, F) floats, required with dbias) and a
+// fixed-order reduce.
+long colwise_ws_floats(int M, int N);
+hipError_t launch_gelu_bwd(const void* dg, const void* u, void* du, float* dbias, float* ws, bool bf16,
                            int M, int F, hipStream_t stream);
-// out[N] += colsum(dy[M, N])
-hipError_t launch_colsum_accum(const void* dy, bool bf16, float* out, int M, int N,
+// out[N] += colsum(dy[M, N]); ws: colwise_ws_floats(M, N) floats
+hipError_t launch_colsum_accum(const void* dy, bool bf16, float* out, float* ws, int M, int N,
                                hipStream_t stream);
 // x[b*T+t] = wte[ids] + wpe[t]
 // x = dropout(wte[ids] + wpe[t]); the backward applies the same mask to dx before the scatter
@@ -81,6 +88,24 @@ hipError_t launch_embedding_bwd(const float* dx, const int64_t* ids, float* dwte
                                 int B, int T, int d, int V, DropoutArgs dropout, hipStream_t stream);
 // keep-mask of elements 0..n-1 of one dropout site (tests)
 hipError_t launch_dropout_mask(DropoutArgs dropout, bool* out, long long n, hipStream_t stream);
+
+// ---- fixed-order column sums (csrc/reduce.hip) ------------------------------------------
+// Producers write one partial row per workgroup, parts[p][c] (p < nparts), with plain
+// stores; launch_colsum_reduce adds sum_p parts[p][c] to dst in a fixed order (bitwise
+// reproducible, no contended atomics).  `scratch` holds colsum_scratch_floats(nparts, ncols)
+// floats (none for nparts <= 64).  dst is a [rows][row_len] view with leading dimension
+// dst_ld (row_len <= 0: dst is contiguous, ncols long).
+long colsum_scratch_floats(int nparts, long ncols);
+hipError_t launch_colsum_reduce(const float* parts, int nparts, long ncols, float* dst, float* scratch,
+                                hipStream_t stream, int row_len = 0, long dst_ld = 0);
+// Process-wide deterministic mode (run.deterministic): the weight-gradient GEMM reduces its split-K
+// partial tiles in a fixed order instead of with atomics (the other reductions always do).
+void set_deterministic(bool on);
+bool deterministic();
+// dwte[v] += sum of dx[order[j]] over the run of sorted_ids == v (stable sort of the tokens):
+// one writer per row, fixed order — the deterministic form of launch_embedding_bwd's scatter.
+hipError_t launch_embedding_bwd_sorted(const float* dx, const int64_t* sorted_ids, const int64_t* order, float* dwte,
+                                       int M, int d, int V, DropoutArgs dropout, hipStream_t stream);
 
 // ---- optimizer ---------------------------------------------------------------------------
 struct AdamWArgs {
@@ -103,8 +128,11 @@ hipError_t launch_sumsq(const float* x, long long n, float* partials, float* out
 
 // ---- weight-gradient GEMM: C[N, K] (f32) += dY[M, N]^T X[M, K] (bf16), split-K + atomics --
 // split <= 0 / tile == 0 let the launcher's cost model choose (tile 128 or 256 forces one).
+// Deterministic mode: `det_ws` (wgrad_gemm_det_ws_floats(...) floats) receives per-chunk partial
+// slabs that are reduced into C in a fixed order instead of the split-K atomics.
+long wgrad_gemm_det_ws_floats(int lda, int ldb, int M, int N, int K, int split, int tile);
 hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N,
-                             int K, int split, int tile, hipStream_t stream);
+                             int K, int split, int tile, hipStream_t stream, float* det_ws = nullptr);
 
 // ---- forward / data-gradient GEMM with fused epilogues (bf16 in, fp32 accumulate, bf16 out)
 // C[M, N] = epi(A[M, K] . op(B)); B is [N, ldb] (K contiguous, b_kn = false) or [K, ldb]
@@ -124,12 +152,17 @@ struct GemmFusedArgs {
   const void* u = nullptr;
   int ldu = 0;
   float* dbias = nullptr;
+  float* ws = nullptr;     // with dbias: gemm_fused_ws_floats(M, N) floats of partial column sums
   float* delta = nullptr;  // epilogue 3: per-head row dot products of C and U, [M / T, N / 64, T]
   int T = 0;               // epilogue 3: rows per sequence
   int M = 0, N = 0, K = 0;
   int epilogue = 0;
 };
 hipError_t launch_gemm_fused(const GemmFusedArgs& args, hipStream_t stream);
+inline long gemm_fused_ws_floats(int M, int N) {
+  const int nparts = (M + 127) / 128;
+  return (long)nparts * N + colsum_scratch_floats(nparts, N);
+}
 
 // ---- causal flash attention (head_dim <= 64, multiple of 8) ------------------------------
 // Shape + options shared by the forward and backward launchers.  The kernels are specialised for
@@ -156,8 +189,11 @@ hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, const AttnDim
 long attn_bwd_workspace_floats(int B, int T, int H);
 // delta_ready: `delta` already holds rowsum(dO * O) (the out-proj dX GEMM's epilogue 3, which
 // then also added the V part of `dbias`): the delta pass is skipped
+// `bias_ws` (attn_bwd_bias_ws_floats(B, T, H, hd) floats; required with `dbias`) holds the
+// partial rows of the bias column sums, reduced in a fixed order (launch_colsum_reduce)
+long attn_bwd_bias_ws_floats(int B, int T, int H, int hd);
 hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse,
-                           void* dqkv, float* delta, float* dq_part, float* dbias, const AttnDims& dims,
-                           DropoutArgs dropout, hipStream_t stream, bool delta_ready = false);
+                           void* dqkv, float* delta, float* dq_part, float* dbias, float* bias_ws,
+                           const AttnDims& dims, DropoutArgs dropout, hipStream_t stream, bool delta_ready = false);
 
 }  // namespace llmt

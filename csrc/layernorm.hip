@@ -241,7 +241,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     }
   }
 
-  // Cross-wave reduction of the column partials, then one atomic per column per workgroup.  One
+  // Cross-wave reduction of the column partials, then this workgroup's partial row of each
+  // accumulator (dw, db, dproj point at [gridDim.x][d] partial-row buffers; the launcher sums the
+  // rows in a fixed order — reproducible, and cheaper than an atomic per column per workgroup).  One
   // [kBwdWaves][d] buffer is reused for the 2-3 accumulators in turn: 3x less LDS than a buffer
   // per accumulator (25.6 KB instead of 77 KB at d = 1600), so more workgroups fit on a CU.
   const int nacc = dproj != nullptr ? 3 : 2;
@@ -260,7 +262,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       float acc = 0.f;
 #pragma unroll
       for (int wv2 = 0; wv2 < kBwdWaves; ++wv2) acc += smem[wv2 * d + col];
-      atomicAdd(dst + col, acc);
+      dst[(long)blockIdx.x * d + col] = acc;
     }
   }
 }
@@ -281,7 +283,7 @@ void launch_fwd_c(const LnFwdArgs& a, hipStream_t st) {
 }
 
 template <int MAXC>
-void launch_bwd_c(const LnBwdArgs& a, hipStream_t st) {
+int bwd_grid_c(const LnBwdArgs& a) {
   const size_t shm = (size_t)kBwdWaves * a.d * sizeof(float);
   // a whole number of resident waves of workgroups (a partial extra wave would be a pure tail:
   // every workgroup runs the same number of rows)
@@ -300,23 +302,36 @@ void launch_bwd_c(const LnBwdArgs& a, hipStream_t st) {
     // LLMT_LN_BWD_WAVES: resident waves of workgroups per launch (A/B knob; default 4 for rows of <= 768
     // columns, 1 above: GPT-2 XL d = 1600 measured 80.0k (1) vs 79.7k (4) tok/s).  More
     // than one lets the hardware dispatcher balance rows onto CUs the side stream's weight-
-    // gradient GEMMs free up, at the cost of more column-partial atomics (124M / micro-batch 128
-    // same-box: 1 -> 1.0224M, 2 -> 1.0259M, 4 -> 1.0276M, 8 -> 1.0243M tok/s).
+    // gradient GEMMs free up (124M / micro-batch 128 same-box: 1 -> 1.0224M, 2 -> 1.0259M,
+    // 4 -> 1.0276M, 8 -> 1.0243M tok/s).
     const char* e = std::getenv("LLMT_LN_BWD_WAVES");
     const int waves = e ? std::max(1, std::atoi(e)) : (MAXC <= 3 ? 4 : 1);
     per_cu = (n > 0 ? n : 4) * (cus > 0 ? cus : 256) * waves;
   }
-  const int grid = stride_grid((long long)(a.M + kBwdWaves - 1) / kBwdWaves, 1, per_cu);
+  return stride_grid((long long)(a.M + kBwdWaves - 1) / kBwdWaves, 1, per_cu);
+}
+
+template <int MAXC>
+void launch_bwd_c(const LnBwdArgs& a, hipStream_t st) {
+  const size_t shm = (size_t)kBwdWaves * a.d * sizeof(float);
+  const int grid = bwd_grid_c<MAXC>(a);
+  float* pw = a.ws;
+  float* pb = a.ws + (long)grid * a.d;
+  float* pp = a.dproj != nullptr ? a.ws + 2L * grid * a.d : nullptr;
 #define LN_BWD(TDY, LP)                                                                         \
   hipLaunchKernelGGL((ln_bwd_kernel<MAXC, TDY, LP>), dim3(grid), dim3(256), shm, st,            \
                      (const TDY*)a.dy, a.xs, a.mean, a.rstd, a.w, a.dresid, a.dy_scale, a.dx,    \
-                     (TDY*)a.dx_lp, a.dw, a.db, a.dproj, a.M, a.d, a.dropout)
+                     (TDY*)a.dx_lp, pw, pb, pp, a.M, a.d, a.dropout)
   if (a.dy_bf16) {
     if (a.dx_lp != nullptr) LN_BWD(bf16_raw, true); else LN_BWD(bf16_raw, false);
   } else {
     if (a.dx_lp != nullptr) LN_BWD(float, true); else LN_BWD(float, false);
   }
 #undef LN_BWD
+  float* scratch = a.ws + (long)(a.dproj != nullptr ? 3 : 2) * grid * a.d;
+  launch_colsum_reduce(pw, grid, a.d, a.dw, scratch, st);
+  launch_colsum_reduce(pb, grid, a.d, a.db, scratch, st);
+  if (pp != nullptr) launch_colsum_reduce(pp, grid, a.d, a.dproj, scratch, st);
 }
 
 }  // namespace
@@ -341,9 +356,31 @@ hipError_t launch_add_layernorm_fwd(const LnFwdArgs& a, hipStream_t stream) {
 }
 
 hipError_t launch_layernorm_bwd(const LnBwdArgs& a, hipStream_t stream) {
-  if (a.d % 4 != 0 || a.M <= 0) return hipErrorInvalidValue;
+  if (a.d % 4 != 0 || a.M <= 0 || a.ws == nullptr) return hipErrorInvalidValue;
   LN_DISPATCH(launch_bwd_c, a, stream);
   return hipGetLastError();
+}
+
+namespace {
+template <int MAXC>
+void grid_c(const LnBwdArgs& a, int& out) { out = bwd_grid_c<MAXC>(a); }
+}  // namespace
+
+long layernorm_bwd_ws_floats(const LnBwdArgs& a) {
+  if (a.d % 4 != 0 || a.M <= 0) return 0;
+  int grid = 0;
+  switch ((a.d / 4 + 63) / 64) {
+    case 1: grid_c<1>(a, grid); break;
+    case 2: grid_c<2>(a, grid); break;
+    case 3: grid_c<3>(a, grid); break;
+    case 4: grid_c<4>(a, grid); break;
+    case 5: grid_c<5>(a, grid); break;
+    case 6: grid_c<6>(a, grid); break;
+    case 7: grid_c<7>(a, grid); break;
+    case 8: grid_c<8>(a, grid); break;
+    default: return 0;
+  }
+  return (long)(a.dproj != nullptr ? 3 : 2) * grid * a.d + colsum_scratch_floats(grid, a.d);
 }
 
 }  // namespace llmt

@@ -2,9 +2,9 @@
 """Build a small GPT, print parameter counts and run one forward (reference notebook
 notebooks/gpt_model_smoke.ipynb; its anchor: 118,528 parameters for this config).
 
-On a MI355X it additionally runs the fused engine (hand-written gfx950 kernels, bf16) on a
-head_dim-64 variant (the kernels' specialisation; this config's head_dim 16 trains on the module
-path) and reports the loss gap against the module path on the same weights.
+On a MI355X it additionally runs the fused engine (hand-written gfx950 kernels, bf16) on the same
+model (head_dim 16 runs zero-filled in the 64-wide flash-attention tiles) and reports the loss gap
+against the module path on the same weights.
 
     python examples/gpt_model_smoke.py [--device cuda]
 """
@@ -48,10 +48,8 @@ def main(argv: list[str] | None = None) -> dict:
         "blocks": len(model.blocks),
     }
     if args.device == "cuda":
-        # the fused kernels specialise head_dim 64: same model family at d_model 128 / 2 heads
-        gcfg = {**CFG, "d_model": 128, "n_heads": 2, "dropout": 0.0}
-        fused = GPT(**gcfg).cuda()
-        assert fused.fused_supported() and not model.fused_supported()
+        fused = GPT(**{**CFG, "dropout": 0.0}).cuda()
+        assert fused.fused_supported("cuda")
         ref_loss = F.cross_entropy(fused(ids.cuda()).float().reshape(-1, CFG["vocab_size"]), ids.cuda().reshape(-1))
         fused.prepare_runtime(compute_dtype=torch.bfloat16)
         with torch.no_grad():

@@ -34,6 +34,7 @@ __all__ = [
     "linear_fwd",
     "linear_fwd_gelu",
     "scale",
+    "set_deterministic",
     "sumsq",
 ]
 
@@ -45,6 +46,18 @@ def hip_ops():  # noqa: ANN201 - torch op namespace
 
 def _on_gpu(t: torch.Tensor) -> bool:
     return t.device.type == "cuda"
+
+
+def set_deterministic(on: bool) -> bool:
+    """Process-wide deterministic mode of the HIP kernels (``run.deterministic`` on GPU): the
+    split-K weight-gradient GEMM and the embedding token gradient switch from float atomics to
+    fixed-order reductions (every other reduction is fixed-order always).  Returns the previous
+    setting.  The CPU reference ops are deterministic anyway."""
+    if not _ext.load():
+        return False
+    prev = bool(torch.ops.llmtrain_hip.get_deterministic())
+    torch.ops.llmtrain_hip.set_deterministic(bool(on))
+    return prev
 
 
 def add_layernorm_fwd(x, delta, weight, bias, eps: float, out_dtype: torch.dtype, dropout=(0.0, 0)):

@@ -176,6 +176,12 @@ class Trainer:
         self._policy = policy
         self._device = self._policy.device
         self.tuned_gemms = enable_tuned_gemms(self._device)  # shipped hipBLASLt solution table (GPU)
+        if self._device.type == "cuda":
+            # run.deterministic: fixed-order reductions in every HIP kernel (bitwise-reproducible
+            # steps and resumes); false = the split-K / scatter atomics of the fast path
+            from llmtrain import ops
+
+            ops.set_deterministic(cfg.run.deterministic)
         model = model.to(self._device)
         if self._policy.use_fused:
             model.prepare_runtime(compute_dtype=self._policy.compute_dtype)

@@ -61,6 +61,7 @@ CASES = [
     (1, 70, 1, 64, None),
     (3, 300, 4, 64, "mixed"),
     (3, 256, 8, 48, "mixed"),
+    (4, 128, 8, 32, "mixed"),  # the K8s ConfigMap model's attention with padding
     (2, 1024, 12, 64, "mixed"),
 ]
 

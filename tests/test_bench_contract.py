@@ -37,7 +37,7 @@ def test_every_rank_gets_full_micro_batches(world: int, mb: int, accum: int) -> 
     bench = _bench()
     args = argparse.Namespace(model="gpt2-124m", micro_batch=mb, grad_accum=accum, dropout=0.0,
                               path="fused", warmup=1, steps=2, bucket_mb=64.0, device="cuda",
-                              grad_reduce_dtype="fp32")
+                              grad_reduce_dtype="fp32", deterministic=False)
     cfg = bench.make_config(args, world)
     n = cfg.data.extra["train_sequences"]
     assert n // world >= mb * accum

@@ -1,0 +1,140 @@
+"""Deterministic mode (``run.deterministic``) on the GPU: every reduction of the HIP kernels runs in
+a fixed order, so repeated launches on the same inputs are BITWISE identical, whole fused training
+steps too, and a mid-run resume reproduces the uninterrupted run to the reference's tolerance
+(reference tests/test_checkpoint.py:301-320: <= 1e-5).  The fixed-order column sums (bias
+gradients, LayerNorm dgamma/dbeta, qkv-bias in the attention backward) are always on; the
+split-K weight gradient and the embedding token gradient switch from atomics to fixed-order
+reductions only in deterministic mode."""
+
+from __future__ import annotations
+
+import copy
+
+import pytest
+import torch
+
+from llmtrain import ops
+from llmtrain.models.gpt import GPT
+
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("gpu_device")]
+
+
+def hip():
+    return torch.ops.llmtrain_hip
+
+
+@pytest.fixture
+def deterministic():
+    prev = ops.set_deterministic(True)
+    yield
+    ops.set_deterministic(prev)
+
+
+def _rand(shape, seed, dtype=torch.float32, scale=1.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (scale * torch.randn(*shape, generator=g)).to("cuda", dtype)
+
+
+def test_wgrad_deterministic_slabs(deterministic) -> None:
+    M, N, K = 8192, 3072, 768
+    dy, x = _rand((M, N), 1, torch.bfloat16), _rand((M, K), 2, torch.bfloat16)
+    outs = []
+    for _ in range(2):
+        c = _rand((N, K), 3)
+        hip().wgrad_gemm(dy, x, c, 0, 0)
+        outs.append(c)
+    assert torch.equal(outs[0], outs[1])
+    want = _rand((N, K), 3) + dy.float().t() @ x.float()
+    torch.testing.assert_close(outs[0], want, atol=1e-3 * want.abs().max().item(), rtol=1e-3)
+
+
+def test_wgrad_deterministic_lm_head_column_slice(deterministic) -> None:
+    """The LM head's case: N = 50257 columns inside 50304-wide rows, C with its own row stride."""
+    M, N, lda, K = 4096, 50257, 50304, 768
+    dy_full, x = _rand((M, lda), 4, torch.bfloat16), _rand((M, K), 5, torch.bfloat16)
+    dy = dy_full[:, :N]
+    c1, c2 = torch.zeros(N, K, device="cuda"), torch.zeros(N, K, device="cuda")
+    hip().wgrad_gemm(dy, x, c1, 0, 0)
+    hip().wgrad_gemm(dy, x, c2, 0, 0)
+    assert torch.equal(c1, c2)
+    want = dy.float().t() @ x.float()
+    torch.testing.assert_close(c1, want, atol=1e-3 * want.abs().max().item(), rtol=1e-3)
+
+
+def test_embedding_bwd_sorted(deterministic) -> None:
+    B, T, d, V = 8, 512, 768, 3000
+    g = torch.Generator(device="cpu").manual_seed(6)
+    ids = torch.randint(0, V, (B, T), generator=g)
+    ids[0, :100] = 7  # a long run of one token
+    ids = ids.to("cuda")
+    dx = _rand((B * T, d), 7)
+    res = []
+    for _ in range(2):
+        dwte, dwpe = torch.zeros(V, d, device="cuda"), torch.zeros(T, d, device="cuda")
+        hip().embedding_bwd(dx, ids, dwte, dwpe, 0.1, 1234)
+        res.append((dwte, dwpe))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    from llmtrain.ops import reference as ref
+
+    dwte_r, dwpe_r = torch.zeros(V, d, device="cuda"), torch.zeros(T, d, device="cuda")
+    ref.embedding_bwd(dx, ids, dwte_r, dwpe_r, 0.1, 1234)
+    torch.testing.assert_close(res[0][0], dwte_r, atol=1e-4, rtol=1e-5)
+    torch.testing.assert_close(res[0][1], dwpe_r, atol=1e-4, rtol=1e-5)
+
+
+def test_column_sums_are_bitwise_reproducible() -> None:
+    """Bias-gradient reductions (fixed-order partial rows, no atomics) in the default mode too."""
+    M, F = 20000, 3072
+    u, dg = _rand((M, F), 8, torch.bfloat16), _rand((M, F), 9, torch.bfloat16)
+    a = torch.zeros(F, device="cuda")
+    b = torch.zeros(F, device="cuda")
+    hip().gelu_bwd(dg, u, a)
+    hip().gelu_bwd(dg, u, b)
+    assert torch.equal(a, b)
+    x = _rand((M, 768), 10)
+    dy = _rand((M, 768), 11, torch.bfloat16)
+    w = 1 + 0.1 * _rand((768,), 12)
+    from llmtrain.ops import reference as ref
+
+    _, _, mu, rs = ref.add_layernorm_fwd(x, None, w, torch.zeros_like(w), 1e-5, torch.float32)
+    outs = []
+    for _ in range(2):
+        dw, db, dp = torch.zeros(768, device="cuda"), torch.zeros(768, device="cuda"), torch.zeros(768, device="cuda")
+        hip().layernorm_bwd(dy, x, mu, rs, w, None, dw, db, None, True, dp)
+        outs.append(torch.cat([dw, db, dp]))
+    assert torch.equal(outs[0], outs[1])
+    B, T, H = 8, 1024, 12
+    qkv = _rand((B * T, 3 * H * 64), 13, torch.bfloat16)
+    out, lse = hip().attn_fwd(qkv, B, T, H)
+    dout = _rand((B * T, H * 64), 14, torch.bfloat16)
+    biases = []
+    for _ in range(2):
+        db = torch.zeros(3 * H * 64, device="cuda")
+        hip().attn_bwd(dout, qkv, out, lse, B, T, H, 0.0, 0, db)
+        biases.append(db)
+    assert torch.equal(biases[0], biases[1])
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.1])
+def test_fused_step_bitwise_reproducible(deterministic, dropout) -> None:
+    """Two fused forward+backward passes from the same weights, batch and dropout seed produce the
+    same loss and the same flat gradient buffer bit for bit (side stream, split-K, attention,
+    LayerNorm, embedding reductions all fixed-order)."""
+    torch.manual_seed(0)
+    base = GPT(vocab_size=50257, block_size=256, d_model=768, n_layers=2, n_heads=12, d_ff=3072, dropout=dropout)
+    base = base.to("cuda")
+    ids = torch.randint(0, 50257, (8, 256), device="cuda")
+    grads, losses = [], []
+    for _ in range(2):
+        m = copy.deepcopy(base)
+        engine = m.prepare_runtime(compute_dtype=torch.bfloat16)
+        m.train()
+        torch.manual_seed(123)  # same dropout step seed
+        engine.store.zero_grad()
+        loss = m.fused_loss(ids, torch.roll(ids, -1, dims=1))
+        loss.backward()
+        torch.cuda.synchronize()
+        grads.append(engine.store.grad.clone())
+        losses.append(loss.item())
+    assert losses[0] == losses[1]
+    assert torch.equal(grads[0], grads[1])

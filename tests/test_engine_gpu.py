@@ -154,8 +154,9 @@ def _gpu_cfg(root: str, max_steps: int, dropout: float = 0.0) -> RunConfig:
 def test_fused_engine_mid_run_resume(gpu_device, tmp_path, dropout):
     """BASELINE config 5's mid-run checkpoint + --resume on the fused engine (with grad accumulation
     and, optionally, fused dropout whose masks derive from the checkpointed torch RNG state): the
-    resumed run continues the interrupted one.  fp32 atomics in the weight-gradient kernels make
-    bf16 runs non-bitwise, hence a small tolerance instead of the CPU test's 1e-5."""
+    resumed run continues the interrupted one.  ``run.deterministic`` (default true) makes every
+    kernel reduction fixed-order, so the tolerance is the reference's own 1e-5
+    (tests/test_checkpoint.py:301-320)."""
     from llmtrain.training.trainer import Trainer
 
     full = Trainer(_gpu_cfg(str(tmp_path / "a"), 8, dropout), run_dir=tmp_path / "a" / "run").fit()
@@ -165,4 +166,5 @@ def test_fused_engine_mid_run_resume(gpu_device, tmp_path, dropout):
         resume_from=str(part / "checkpoints")
     )
     assert resumed.resumed_from_step == 6 and resumed.final_step == 8
-    assert abs(resumed.final_loss - full.final_loss) <= 2e-3 * abs(full.final_loss)
+    print(f"resume: full {full.final_loss!r} resumed {resumed.final_loss!r}")
+    assert abs(resumed.final_loss - full.final_loss) <= 1e-5 * abs(full.final_loss)

@@ -10,6 +10,12 @@
 
 #include "kernels.h"
 
+#ifdef LLMT_ATTN_PROBE
+namespace llmt {
+void attn_probe_set(unsigned long long* buf);
+}
+#endif
+
 #define CHECK(x)                                                                     \
   do {                                                                               \
     hipError_t e_ = (x);                                                             \
@@ -56,6 +62,53 @@ int main(int argc, char** argv) {
     ms.push_back(t);
   }
   std::sort(ms.begin(), ms.end());
+#ifdef LLMT_ATTN_PROBE
+  {  // per-step cycle anatomy of the (b, h) = 0 workgroups (stamps: csrc/attention_fwd.hip)
+    const int nqb = (T + 127) / 128, nev = 64;
+    const size_t nwg = (size_t)nqb * B * H;
+    const size_t n = (size_t)nqb * 4 * nev + 4 * nwg;
+    unsigned long long* dprobe;
+    CHECK(hipMalloc(&dprobe, n * 8));
+    CHECK(hipMemset(dprobe, 0, n * 8));
+    llmt::attn_probe_set(dprobe);
+    CHECK(llmt::launch_attn_fwd(qkv, out, lse, dims, llmt::DropoutArgs{}, 0));
+    CHECK(hipDeviceSynchronize());
+    std::vector<unsigned long long> p(n);
+    CHECK(hipMemcpy(p.data(), dprobe, n * 8, hipMemcpyDeviceToHost));
+    {  // whole grid: 100 MHz real-time span, shader clock (memtime / realtime), concurrency, WG durations
+      const unsigned long long* wg = &p[(size_t)nqb * 4 * nev];
+      unsigned long long r0 = ~0ull, r1 = 0;
+      double cyc = 0, real = 0;
+      std::vector<double> dur(nqb, 0.0);
+      for (size_t i = 0; i < nwg; ++i) {
+        const unsigned long long* e = &wg[4 * i];
+        r0 = std::min(r0, e[2]);
+        r1 = std::max(r1, e[3]);
+        cyc += (double)(e[1] - e[0]);
+        real += (double)(e[3] - e[2]);
+        dur[nqb - 1 - (int)(i % nqb)] += (double)(e[1] - e[0]);
+      }
+      std::printf("grid span %.1f us (100 MHz realtime) vs %.1f us event-timed; shader clock %.2f GHz; "
+                  "%.1f workgroups resident on average\n",
+                  (r1 - r0) / 100.0, ms[ms.size() / 2] * 1e3, cyc / real * 0.1,
+                  real / (double)(r1 - r0));
+      for (int qb = 0; qb < nqb; ++qb) std::printf("  qb=%d mean WG duration %.0f cycles\n", qb, dur[qb] / (B * H));
+    }
+    for (int qb = 0; qb < nqb; ++qb)
+      for (int w = 0; w < 4; ++w) {
+        const unsigned long long* e = &p[((size_t)qb * 4 + w) * nev];
+        std::printf("probe qb=%d w=%d total=%llu prologue=%llu steps(compute/barrier):", qb, w, e[63] - e[0],
+                    e[1] - e[0]);
+        unsigned long long prev = e[1];
+        for (int it = 0; it < 30 && e[3 + 2 * it] != 0; ++it) {
+          const unsigned long long c = e[2 + 2 * it] ? e[2 + 2 * it] - prev : 0;
+          std::printf(" %llu/%llu", c, e[3 + 2 * it] - (e[2 + 2 * it] ? e[2 + 2 * it] : prev));
+          prev = e[3 + 2 * it];
+        }
+        std::printf(" tail=%llu\n", e[63] - prev);
+      }
+  }
+#endif
   const double flops = 4.0 * B * H * (double)T * T * D / 2;
   std::printf("{\"kernel\": \"attn_fwd\", \"variant\": \"%s\", \"B\": %d, \"ms\": %.4f, \"TFLOPs\": %.1f}\n",
               argc > 2 ? argv[2] : "?", B, ms[ms.size() / 2], flops / ms[ms.size() / 2] / 1e9);

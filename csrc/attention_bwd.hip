@@ -17,7 +17,7 @@
 //    same LDS images that serve the row reads (one swizzle, conflict free both ways);
 //  * dS crosses LDS once (as a [key][q] image written 8 bytes per lane) and dQ = dS K is formed
 //    with 16x16x32 MFMAs over the block's 256 keys (K^T LDS image, one ds_read_b128 per B
-//    operand); each key block stores its dQ contribution to its OWN fp32 partial plane with
+//    operand); each key block stores its dQ contribution to its OWN bf16 partial plane with
 //    plain stores (4-5x the chip-wide float-atomic rate, and no memset), and a reduce pass sums
 //    the <= T/256 planes per row straight into the packed bf16 dqkv;
 //  * branch-free buffer loads (rows past T read as zero), double-buffered Q/dO and dS images,
@@ -106,7 +106,8 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
   }
 }
 
-// dqkv[b, t, 0, h, :] = bf16(sum over key blocks kb <= t / 256 of dq_part[kb][b, h, t, :]):
+// dqkv[b, t, 0, h, :] = bf16(sum over key blocks kb <= t / 256 of dq_part[kb][b, h, t, :]) with
+// bf16 partial planes summed in fp32:
 // the main kernel stores each key block's dQ contribution with plain stores (no memset, no
 // atomics); rows only ever read the partials their causal key blocks wrote.  A workgroup owns
 // kDqRows rows t of one (b, h) inside one 256-key block, so all its rows sum the same number of
@@ -115,7 +116,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
 // qparts[b * gridDim.y + tile][h * hd + d] (fixed-order reduce afterwards, no atomics).
 constexpr int kDqRows = 64;
 template <bool SMALLHD>
-__global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const float* __restrict__ part, bf16_raw* __restrict__ dqkv,
+__global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const bf16_raw* __restrict__ part, bf16_raw* __restrict__ dqkv,
                                                              float* __restrict__ qparts, int T, int H, int hd_arg,
                                                              int nkb, long plane) {
   const int hd = SMALLHD ? hd_arg : kHD;
@@ -127,7 +128,7 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const float* __rest
   const int t0 = tile * kDqRows + rl;  // this thread's rows: t0 + 32 * it
   const int last = min(tile * kDqRows / kKvBlk, nkb - 1);
   constexpr int kSweeps = kDqRows / 32;
-  // key-block planes outermost: each plane step issues all 16 loads of the thread's 8 rows at
+  // key-block planes outermost: each plane step issues all 8 loads of the thread's 8 rows at
   // once (rows past T re-read row T - 1, which every plane up to `last` holds; result unused)
   float f[kSweeps][8];
 #pragma unroll
@@ -138,13 +139,10 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const float* __rest
 #pragma unroll
     for (int it = 0; it < kSweeps; ++it) {
       const int t = min(t0 + 32 * it, T - 1);
-      const float4_t* src = reinterpret_cast<const float4_t*>(part + kb * plane + ((long)bh * T + t) * kHD + 8 * c);
-      const float4_t x = src[0], y = src[1];
+      float x[8];
+      unpack8(*reinterpret_cast<const ushort8_t*>(part + kb * plane + ((long)bh * T + t) * kHD + 8 * c), x);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        f[it][j] += x[j];
-        f[it][4 + j] += y[j];
-      }
+      for (int j = 0; j < 8; ++j) f[it][j] += x[j];
     }
   }
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -174,16 +172,6 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const float* __rest
     const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
     qparts[((long)b * gridDim.y + tile) * (H * hd) + h * hd + threadIdx.x] = s;
   }
-}
-
-// raw 16-byte / 4-byte buffer loads: offsets past the descriptor's record count read as zero
-__device__ __forceinline__ ushort8_t buf_load16(__amdgpu_buffer_rsrc_t r, int byte_off) {
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
-  return __builtin_bit_cast(ushort8_t, v);
-}
-__device__ __forceinline__ float buf_load_f32(__amdgpu_buffer_rsrc_t r, int byte_off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
 }
 
 // K^T image [64 d][256 keys]: 512-byte rows, 16-byte chunk index XOR-swizzled by (d & 15) so the
@@ -425,17 +413,26 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
         acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b0, acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b1, acc1, 0, 0, 0);
       }
-      // this key block's dQ contribution -> its own fp32 partial plane (plain stores, 64-byte
-      // row segments per 16 lanes); attn_dq_reduce_kernel sums the planes
-      const int d0 = 32 * dp_dq + i;
-      float* plane = dq_part + ((long)kb * gridDim.x + bh) * T * kHD;
+      // this key block's dQ contribution -> its own bf16 partial plane (plain stores; the planes
+      // are the largest traffic of the backward: bf16 halves the bytes written here and read by
+      // attn_dq_reduce_kernel, which sums them in fp32).  Lanes i and i^1 swap half their rows so
+      // each lane stores whole dwords (two adjacent columns): even lanes rows 0,1, odd rows 2,3.
+      const int p = i & 1;
+      const int dcol = 32 * dp_dq + (i & ~1);  // even column of this lane's pair
+      bf16_raw* plane = reinterpret_cast<bf16_raw*>(dq_part) + ((long)kb * gridDim.x + bh) * T * kHD;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int j = 0; j < 2; ++j) {
+        const int r = p ? 2 + j : j;  // the row this lane stores
         const int qq = q0 + 16 * qt_dq + 4 * g + r;
+        const float s0 = __shfl_xor(p ? acc0[j] : acc0[2 + j], 1, 64);
+        const float s1 = __shfl_xor(p ? acc1[j] : acc1[2 + j], 1, 64);
+        const float o0 = p ? acc0[2 + j] : acc0[j], o1 = p ? acc1[2 + j] : acc1[j];
+        const uint32_t w0 = (uint32_t)f2bf((p ? s0 : o0) * scale) | ((uint32_t)f2bf((p ? o0 : s0) * scale) << 16);
+        const uint32_t w1 = (uint32_t)f2bf((p ? s1 : o1) * scale) | ((uint32_t)f2bf((p ? o1 : s1) * scale) << 16);
         if (qq < T) {
-          float* dst = plane + (long)qq * kHD + d0;
-          dst[0] = acc0[r] * scale;
-          dst[16] = acc1[r] * scale;
+          bf16_raw* dst = plane + (long)qq * kHD + dcol;
+          *reinterpret_cast<uint32_t*>(dst) = w0;
+          *reinterpret_cast<uint32_t*>(dst + 16) = w1;
         }
       }
     }
@@ -491,7 +488,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
 
 long attn_bwd_workspace_floats(int B, int T, int H) {
   const long nkb = (T + attn::kKvBlk - 1) / attn::kKvBlk;
-  return nkb * B * H * (long)T * attn::kHD;
+  return (nkb * B * H * (long)T * attn::kHD + 1) / 2;  // bf16 planes
 }
 
 namespace {
@@ -559,7 +556,7 @@ hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, c
   }
   const dim3 rgrid(B * H, (T + attn::kDqRows - 1) / attn::kDqRows);
   hipLaunchKernelGGL(small ? attn::attn_dq_reduce_kernel<true> : attn::attn_dq_reduce_kernel<false>, rgrid, dim3(256),
-                     0, stream, dq_part, dq, qparts, T, H, hd, nkb, rows * (long)attn::kHD);
+                     0, stream, (const bf16_raw*)dq_part, dq, qparts, T, H, hd, nkb, rows * (long)attn::kHD);
   if (dbias != nullptr) {
     // fixed-order sums of the partial rows: Q part, then (unless the out-proj GEMM's epilogue
     // already added it) the V part; the K part of the qkv-bias gradient is exactly zero

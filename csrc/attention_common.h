@@ -34,6 +34,16 @@ __device__ __forceinline__ int tile_elem_off(int row, int col) {
   return row * kHD + (swz(row, col >> 3) << 3) + (col & 7);
 }
 
+// raw 16-byte / 4-byte buffer loads: offsets past the descriptor's record count read as zero
+__device__ __forceinline__ ushort8_t buf_load16(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
+  return __builtin_bit_cast(ushort8_t, v);
+}
+__device__ __forceinline__ float buf_load_f32(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
+
 // 8 contiguous bf16 of one row (an MFMA A/B fragment with k along the row)
 __device__ __forceinline__ bf16x8 lds_row_read(const bf16_raw* tile, int row, int ch) {
   return *reinterpret_cast<const bf16x8*>(tile + tile_chunk_off(row, ch));

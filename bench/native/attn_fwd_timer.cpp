@@ -86,7 +86,7 @@ int main(int argc, char** argv) {
         r1 = std::max(r1, e[3]);
         cyc += (double)(e[1] - e[0]);
         real += (double)(e[3] - e[2]);
-        dur[nqb - 1 - (int)(i % nqb)] += (double)(e[1] - e[0]);
+        dur[(int)(i % nqb)] += (double)(e[1] - e[0]);
       }
       std::printf("grid span %.1f us (100 MHz realtime) vs %.1f us event-timed; shader clock %.2f GHz; "
                   "%.1f workgroups resident on average\n",

@@ -44,16 +44,16 @@ namespace attn {
 // the prologue, 2 + 2 it after step it's compute, 3 + 2 it after its barrier, 63 exit.
 __device__ unsigned long long* g_attn_probe = nullptr;  // null: no stamps
 // Every workgroup's wave 0 also stores its entry / exit stamps (events 0 / 63) to
-// g_attn_probe[nqb * kFwdWaves * 64 + 4 * (blockIdx.y * nqb + blockIdx.x) + {0, 1}] (s_memtime) and
+// g_attn_probe[nqb * kFwdWaves * 64 + 4 * (bh * nqb + qb) + {0, 1}] (s_memtime) and
 // + {2, 3} (s_memrealtime: 100 MHz, one clock for the whole chip).
 #define ATTN_PROBE(ev)                                                                                   \
   do {                                                                                                   \
     if (g_attn_probe != nullptr && (threadIdx.x & 63) == 0) {                                            \
       const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                        \
-      if (blockIdx.y == 0 && (ev) < 64)                                                                  \
-        g_attn_probe[((long)(nqb - 1 - (int)blockIdx.x) * kFwdWaves + (threadIdx.x >> 6)) * 64 + (ev)] = t_; \
+      if (blockIdx.x == 0 && (ev) < 64)                                                                  \
+        g_attn_probe[((long)(nqb - 1 - (int)blockIdx.y) * kFwdWaves + (threadIdx.x >> 6)) * 64 + (ev)] = t_; \
       if (threadIdx.x == 0 && ((ev) == 0 || (ev) == 63)) {                                               \
-        unsigned long long* g_ = g_attn_probe + (long)nqb * kFwdWaves * 64 + 4 * ((long)blockIdx.y * nqb + blockIdx.x); \
+        unsigned long long* g_ = g_attn_probe + (long)nqb * kFwdWaves * 64 + 4 * ((long)blockIdx.x * nqb + nqb - 1 - blockIdx.y); \
         g_[(ev) == 63] = t_;                                                                             \
         g_[2 + ((ev) == 63)] = __builtin_amdgcn_s_memrealtime();                                         \
       }                                                                                                  \
@@ -95,8 +95,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
   // wave-uniform, so hipcc emits scalar branches instead of per-lane exec-mask control flow
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int half = lane >> 5, col = lane & 31;
-  const int qb = nqb - 1 - (int)blockIdx.x;  // heavy blocks first
-  const int bh = blockIdx.y;
+  // grid (B*H, nqb), x fastest: dispatch runs through ALL (b, h) of the heaviest (last) query
+  // block first, so the grid ends on the lightest blocks instead of a tail of heavy ones (with
+  // (b, h) outermost the last-dispatched heavy blocks left ~40% of the workgroup slots idle at the
+  // end: 315 of 512 resident on average, bench/native/attn_fwd_timer probe).  All blocks of one
+  // (b, h) land on the same XCD (B*H is a multiple of 8 at the model shapes), sharing K/V in L2.
+  const int qb = nqb - 1 - (int)blockIdx.y;
+  const int bh = blockIdx.x;
   const int b = bh / H, h = bh - b * H;
   const int hd = SMALLHD ? hd_arg : kHD;  // head dim in memory; tiles stay 64 wide
   const long row_stride = 3L * H * hd;   // elements between consecutive tokens in qkv
@@ -399,7 +404,7 @@ hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, const AttnDim
   if (d.B <= 0 || d.T <= 0 || d.H <= 0 || d.T > 65535 || d.hd <= 0 || d.hd > attn::kHD || d.hd % 8 != 0)
     return hipErrorInvalidValue;
   const int nqb = (d.T + attn::kQBlk - 1) / attn::kQBlk;
-  dim3 grid(nqb, d.B * d.H);
+  dim3 grid(d.B * d.H, nqb);
   const bool drop = dropout.thr != 0, km = d.key_bits != nullptr, small = d.hd != attn::kHD;
   const int variant = (drop ? 4 : 0) | (km ? 2 : 0) | (small ? 1 : 0);
   auto q = (const bf16_raw*)qkv;

@@ -13,6 +13,12 @@
 
 #include "kernels.h"
 
+#ifdef LLMT_ATTN_PROBE
+namespace llmt {
+void attn_bwd_probe_set(unsigned long long* buf);
+}
+#endif
+
 #define CHECK(x)                                                              \
   do {                                                                        \
     hipError_t e_ = (x);                                                      \
@@ -68,6 +74,48 @@ int main(int argc, char** argv) {
     ms.push_back(t);
   }
   std::sort(ms.begin(), ms.end());
+#ifdef LLMT_ATTN_PROBE
+  {  // per-tile cycle anatomy of the (b, h) = 0 workgroups + whole-grid residency (attention_bwd.hip)
+    const int nkb = (T + 255) / 256, nev = 64;
+    const size_t nwg = (size_t)nkb * B * H;
+    const size_t n = (size_t)nkb * 8 * nev + 4 * nwg;
+    unsigned long long* dprobe;
+    CHECK(hipMalloc(&dprobe, n * 8));
+    CHECK(hipMemset(dprobe, 0, n * 8));
+    llmt::attn_bwd_probe_set(dprobe);
+    CHECK(llmt::launch_attn_bwd(dout, qkv, out, lse, dqkv, delta, dq, nullptr, nullptr, dims, llmt::DropoutArgs{}, 0));
+    CHECK(hipDeviceSynchronize());
+    std::vector<unsigned long long> p(n);
+    CHECK(hipMemcpy(p.data(), dprobe, n * 8, hipMemcpyDeviceToHost));
+    const unsigned long long* wg = &p[(size_t)nkb * 8 * nev];
+    unsigned long long r0 = ~0ull, r1 = 0;
+    double cyc = 0, real = 0;
+    std::vector<double> dur(nkb, 0.0);
+    for (size_t i = 0; i < nwg; ++i) {
+      const unsigned long long* e = &wg[4 * i];
+      r0 = std::min(r0, e[2]);
+      r1 = std::max(r1, e[3]);
+      cyc += (double)(e[1] - e[0]);
+      real += (double)(e[3] - e[2]);
+      dur[i % nkb] += (double)(e[1] - e[0]);
+    }
+    std::printf("grid span %.1f us (100 MHz realtime); shader clock %.2f GHz; %.1f workgroups resident on average\n",
+                (r1 - r0) / 100.0, cyc / real * 0.1, real / (double)(r1 - r0));
+    for (int kb = 0; kb < nkb; ++kb) std::printf("  kb=%d mean WG duration %.0f cycles\n", kb, dur[kb] / (B * H));
+    for (int kb = 0; kb < nkb; ++kb)
+      for (int w = 0; w < 8; w += 7) {
+        const unsigned long long* e = &p[((size_t)kb * 8 + w) * nev];
+        std::printf("probe kb=%d w=%d total=%llu prologue=%llu tiles(phaseA/stage+barrier/dQ):", kb, w, e[63] - e[0],
+                    e[1] - e[0]);
+        unsigned long long prev = e[1];
+        for (int it = 0; it < 20 && e[4 + 3 * it] != 0; ++it) {
+          std::printf(" %llu/%llu/%llu", e[2 + 3 * it] - prev, e[3 + 3 * it] - e[2 + 3 * it], e[4 + 3 * it] - e[3 + 3 * it]);
+          prev = e[4 + 3 * it];
+        }
+        std::printf(" tail=%llu\n", e[63] - prev);
+      }
+  }
+#endif
   const double flops = 2.5 * 4.0 * B * H * (double)T * T * D / 2;
   std::printf("{\"kernel\": \"attn_bwd\", \"variant\": \"%s\", \"B\": %d, \"ms\": %.4f, \"TFLOPs\": %.1f}\n",
               argc > 2 ? argv[2] : "?", B, ms[ms.size() / 2], flops / ms[ms.size() / 2] / 1e9);

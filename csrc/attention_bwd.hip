@@ -33,6 +33,31 @@ namespace llmt {
 namespace attn {
 
 constexpr int kBwdWaves = 8;
+
+#ifdef LLMT_ATTN_PROBE
+// Timing probe (bench/native/attn_bwd_timer.cpp with -DLLMT_ATTN_PROBE): lane 0 of each wave of the
+// (b, h) = 0 workgroups stores s_memtime stamps [kb][wave][event]: 0 entry, 1 after the prologue,
+// then per query tile it: 2 + 3 it after phase A, 3 + 3 it after the staging store + barrier,
+// 4 + 3 it after the dQ phase; 63 exit.  Every workgroup's wave 0 stores entry / exit as
+// s_memtime and s_memrealtime at g_attn_bwd_probe[nkb * kBwdWaves * 64 + 4 * (bh * nkb + kb)].
+__device__ unsigned long long* g_attn_bwd_probe = nullptr;
+#define BWD_PROBE(ev)                                                                                    \
+  do {                                                                                                   \
+    if (g_attn_bwd_probe != nullptr && (threadIdx.x & 63) == 0) {                                        \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                        \
+      if (blockIdx.x == 0 && (ev) < 64) g_attn_bwd_probe[((long)kb * kBwdWaves + wave) * 64 + (ev)] = t_; \
+      if (threadIdx.x == 0 && ((ev) == 0 || (ev) == 63)) {                                               \
+        unsigned long long* g_ = g_attn_bwd_probe + (long)nkb * kBwdWaves * 64 + 4 * ((long)bh * nkb + kb); \
+        g_[(ev) == 63] = t_;                                                                             \
+        g_[2 + ((ev) == 63)] = __builtin_amdgcn_s_memrealtime();                                         \
+      }                                                                                                  \
+    }                                                                                                    \
+  } while (0)
+#else
+#define BWD_PROBE(ev) \
+  do {                \
+  } while (0)
+#endif
 constexpr int kKvBlk = 32 * kBwdWaves;  // 256 keys per workgroup
 constexpr int kQTile = 64;  // query rows per sweep step (two 32-row MFMA tiles)
 
@@ -376,9 +401,11 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
     }
   };
 
+  BWD_PROBE(0);
   load_tile(kblk0);
   store_tile(0);
   __syncthreads();
+  BWD_PROBE(1);
 
   int it = 0;
   for (int q0 = kblk0; q0 < T; q0 += kQTile, ++it) {
@@ -389,10 +416,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
     const bf16_raw* do_lds = qd_lds[cur][1];
     bf16_raw* dsimg = ds_lds[cur];
     phase_a(q0 >= kblk0 + kKvBlk && q0 + kQTile <= T, q0, q_lds, do_lds, rowc_lds[cur], dsimg);
+    BWD_PROBE(2 + 3 * it);
     if (more) store_tile(cur ^ 1);
     // one barrier per tile: the dS image and the next Q/dO tile are double-buffered, so the only
     // hand-off is "phase A of this tile (and the next tile's staging) done by every wave"
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    BWD_PROBE(3 + 3 * it);
 
     // ---- dQ[q0 + 16 qt .., 32 dp + (0..31)] += dS K over the block's 256 keys (16x16x32) ----
     {
@@ -436,6 +465,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
         }
       }
     }
+    BWD_PROBE(4 + 3 * it);
   }
 
   // ---- dK = scale * dK^T, dV = dV^T  -> dqkv[b, key, 1|2, h, :] ------------------------------
@@ -464,6 +494,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   // delta kernel's column sums of dO.  V with dropout (rows of the dropped P no longer sum to 1):
   // sum this block's 256 keys of dV^T — over the 32 lanes of each half, then over the 8 waves —
   // into this block's partial row vparts[b * nkb + kb][h * hd + d].
+  BWD_PROBE(63);
   if (!DROPOUT || vparts == nullptr) return;
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt) {
@@ -510,6 +541,12 @@ long attn_bwd_bias_ws_floats(int B, int T, int H, int hd) {
   const long sv = colsum_scratch_floats(p.nv, p.cols), sq = colsum_scratch_floats(p.nq, p.cols);
   return (long)(p.nv + p.nq) * p.cols + (sv > sq ? sv : sq);
 }
+
+#ifdef LLMT_ATTN_PROBE
+void attn_bwd_probe_set(unsigned long long* buf) {
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(attn::g_attn_bwd_probe), &buf, sizeof(buf));
+}
+#endif
 
 template <bool DROPOUT, bool KMASK, bool SMALLHD>
 static void launch_bwd_variant(dim3 grid, hipStream_t stream, const bf16_raw* qkv, const bf16_raw* dout,

@@ -93,11 +93,15 @@ hipError_t launch_dropout_mask(DropoutArgs dropout, bool* out, long long n, hipS
 // Producers write one partial row per workgroup, parts[p][c] (p < nparts), with plain
 // stores; launch_colsum_reduce adds sum_p parts[p][c] to dst in a fixed order (bitwise
 // reproducible, no contended atomics).  `scratch` holds colsum_scratch_floats(nparts, ncols)
-// floats (none for nparts <= 64).  dst is a [rows][row_len] view with leading dimension
+// floats (none for nparts <= 256).  dst is a [rows][row_len] view with leading dimension
 // dst_ld (row_len <= 0: dst is contiguous, ncols long).
 long colsum_scratch_floats(int nparts, long ncols);
 hipError_t launch_colsum_reduce(const float* parts, int nparts, long ncols, float* dst, float* scratch,
                                 hipStream_t stream, int row_len = 0, long dst_ld = 0);
+// njobs (<= 4) reductions of the same nparts x ncols shape in one launch per level; `scratch`
+// holds njobs * colsum_scratch_floats(nparts, ncols) floats
+hipError_t launch_colsum_reduce_multi(const float* const* parts, float* const* dst, int njobs, int nparts, long ncols,
+                                      float* scratch, hipStream_t stream, int row_len = 0, long dst_ld = 0);
 // Process-wide deterministic mode (run.deterministic): the weight-gradient GEMM reduces its split-K
 // partial tiles in a fixed order instead of with atomics (the other reductions always do).
 void set_deterministic(bool on);

@@ -328,10 +328,11 @@ void launch_bwd_c(const LnBwdArgs& a, hipStream_t st) {
     if (a.dx_lp != nullptr) LN_BWD(float, true); else LN_BWD(float, false);
   }
 #undef LN_BWD
-  float* scratch = a.ws + (long)(a.dproj != nullptr ? 3 : 2) * grid * a.d;
-  launch_colsum_reduce(pw, grid, a.d, a.dw, scratch, st);
-  launch_colsum_reduce(pb, grid, a.d, a.db, scratch, st);
-  if (pp != nullptr) launch_colsum_reduce(pp, grid, a.d, a.dproj, scratch, st);
+  const int nacc = a.dproj != nullptr ? 3 : 2;
+  float* scratch = a.ws + (long)nacc * grid * a.d;
+  const float* parts[3] = {pw, pb, pp};
+  float* dst[3] = {a.dw, a.db, a.dproj};
+  launch_colsum_reduce_multi(parts, dst, nacc, grid, a.d, scratch, st);
 }
 
 }  // namespace
@@ -380,7 +381,8 @@ long layernorm_bwd_ws_floats(const LnBwdArgs& a) {
     case 8: grid_c<8>(a, grid); break;
     default: return 0;
   }
-  return (long)(a.dproj != nullptr ? 3 : 2) * grid * a.d + colsum_scratch_floats(grid, a.d);
+  const int nacc = a.dproj != nullptr ? 3 : 2;
+  return (long)nacc * grid * a.d + (long)nacc * colsum_scratch_floats(grid, a.d);
 }
 
 }  // namespace llmt

@@ -9,8 +9,11 @@
 //  * and cheaper than contended atomics: the delta / dQ-reduce passes of the attention backward
 //    sent 512-2048 atomic adds to each bias address (MI355X_MICROARCH: same-address atomics
 //    serialise at the memory side).
-// Two levels: groups of G ~ sqrt(nparts) parts -> scratch[g][c] (one thread per column,
-// consecutive threads = consecutive columns, i.e. coalesced 256-byte rows), then the groups -> dst.
+// Workgroup = 64 columns (one per lane: coalesced 256-byte rows) x 4 waves, each wave summing a
+// contiguous quarter of the parts in order, the quarters added in wave order.  Up to 256 parts:
+// one pass into dst; above: groups of 128 parts -> scratch[g][c], then the groups -> dst (two
+// launches, 4 dependent load rounds each).  Several same-shape reductions share one launch
+// (launch_colsum_reduce_multi: LayerNorm backward's 2-3 column sums).
 //
 // embedding_bwd_sorted_kernel: dwte[v] += sum of dx rows whose token is v, over the rows in
 // (stable) sorted-token order: one wave owns each run of equal tokens, so there is one writer
@@ -22,42 +25,59 @@
 namespace llmt {
 namespace {
 
-constexpr int kOneLevel = 64;  // up to this many parts: one pass straight into dst
+constexpr int kStrip = 64;      // columns per workgroup: one per lane, 256-byte coalesced rows
+constexpr int kWaves = 4;       // waves per workgroup, each summing a contiguous quarter of the parts
+constexpr int kOneLevel = 256;  // up to this many parts: one pass straight into dst
+constexpr int kGroup = 128;     // parts per first-level group above that (32 per wave)
 
-// parts summed per first-level thread: ~sqrt(nparts), a multiple of 8, so two levels always do
-int group_size(int nparts) {
-  int g = 8;
-  while ((long)g * g < nparts) g += 8;
-  return g;
-}
+// One job = one (parts, dst, scratch) triple; up to kMaxJobs jobs of the same shape share a
+// launch (blockIdx.z), e.g. LayerNorm backward's dgamma / dbeta / projection-bias rows.
+constexpr int kMaxJobs = 4;
+struct Jobs {
+  const float* parts[kMaxJobs];
+  float* dst[kMaxJobs];
+};
 
-// out[g][c] (+)= sum_{p in group g} parts[p][c]; `accumulate` adds into out (the final level)
-__global__ __launch_bounds__(256) void colsum_parts_kernel(const float* __restrict__ parts, int nparts, int group,
-                                                           long ncols, float* __restrict__ out, int row_len,
-                                                           long out_ld, bool accumulate) {
-  const long c = (long)blockIdx.x * 256 + threadIdx.x;
-  if (c >= ncols) return;
+// out[g][c] (+)= sum_{p in group g} parts[p][c].  Wave w of the workgroup sums its quarter of the
+// group's parts in order (8 loads in flight per lane), the quarters are added in wave order
+// through LDS: a fixed association for a given (nparts, group), hence bitwise reproducible.
+// `accumulate` (final level) adds into column c of a [rows][row_len] view with leading dimension
+// out_ld; otherwise the group's sum is stored to out[g][c].
+__global__ __launch_bounds__(256) void colsum_parts_kernel(Jobs jobs, int nparts, int group, long ncols,
+                                                           int row_len, long out_ld, bool accumulate) {
+  __shared__ float red[kWaves][kStrip];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long c = (long)blockIdx.x * kStrip + lane;
   const int g = blockIdx.y;
+  const float* parts = jobs.parts[blockIdx.z];
   const int p0 = g * group, p1 = min(nparts, p0 + group);
+  const int per = (p1 - p0 + kWaves - 1) / kWaves;
+  const int w0 = min(p1, p0 + wave * per), w1 = min(p1, w0 + per);
   float acc = 0.f;
-  int p = p0;
-  // 8 independent loads in flight per thread, summed in part order
-  for (; p + 8 <= p1; p += 8) {
-    float v[8];
+  if (c < ncols) {
+    int p = w0;
+    for (; p + 8 <= w1; p += 8) {
+      float v[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = parts[(long)(p + i) * ncols + c];
+      for (int i = 0; i < 8; ++i) v[i] = parts[(long)(p + i) * ncols + c];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc += v[i];
+      for (int i = 0; i < 8; ++i) acc += v[i];
+    }
+    for (; p < w1; ++p) acc += parts[(long)p * ncols + c];
   }
-  for (; p < p1; ++p) acc += parts[(long)p * ncols + c];
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave != 0 || c >= ncols) return;
+  const float sum = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  float* out = jobs.dst[blockIdx.z];
   if (accumulate) {
-    // final level: column c of a [rows][row_len] view with leading dimension out_ld
-    const long dst = (c / row_len) * out_ld + c % row_len;
-    out[dst] += acc;
+    out[(c / row_len) * out_ld + c % row_len] += sum;
   } else {
-    out[(long)g * ncols + c] = acc;
+    out[(long)g * ncols + c] = sum;
   }
 }
+
+int num_groups(int nparts) { return nparts <= kOneLevel ? 1 : (nparts + kGroup - 1) / kGroup; }
 
 // rows [i0, i1) of the sorted order with equal tokens: the wave at a run's first row sums it
 __global__ __launch_bounds__(256) void embedding_bwd_sorted_kernel(const float* __restrict__ dx,
@@ -103,32 +123,45 @@ void set_deterministic(bool on) { g_deterministic = on; }
 bool deterministic() { return g_deterministic; }
 
 long colsum_scratch_floats(int nparts, long ncols) {
-  if (nparts <= kOneLevel) return 0;
-  const int g = group_size(nparts);
-  return (long)((nparts + g - 1) / g) * ncols;
+  return nparts <= kOneLevel ? 0 : (long)num_groups(nparts) * ncols;
 }
 
-hipError_t launch_colsum_reduce(const float* parts, int nparts, long ncols, float* dst, float* scratch,
-                                hipStream_t stream, int row_len, long dst_ld) {
-  if (nparts <= 0 || ncols <= 0) return hipSuccess;
+hipError_t launch_colsum_reduce_multi(const float* const* parts, float* const* dst, int njobs, int nparts, long ncols,
+                                      float* scratch, hipStream_t stream, int row_len, long dst_ld) {
+  if (nparts <= 0 || ncols <= 0 || njobs <= 0) return hipSuccess;
+  if (njobs > kMaxJobs) return hipErrorInvalidValue;
   if (row_len <= 0) {
     row_len = (int)ncols;
     dst_ld = ncols;
   }
   const dim3 block(256);
-  const unsigned gx = (unsigned)((ncols + 255) / 256);
-  if (nparts <= kOneLevel) {
-    hipLaunchKernelGGL(colsum_parts_kernel, dim3(gx, 1), block, 0, stream, parts, nparts, nparts, ncols, dst, row_len,
-                       dst_ld, true);
-    return hipGetLastError();
+  const unsigned gx = (unsigned)((ncols + kStrip - 1) / kStrip);
+  Jobs final_jobs{}, first{};
+  const int groups = num_groups(nparts);
+  for (int j = 0; j < njobs; ++j) {
+    final_jobs.dst[j] = dst[j];
+    if (groups == 1) {
+      final_jobs.parts[j] = parts[j];
+    } else {
+      first.parts[j] = parts[j];
+      first.dst[j] = scratch + (long)j * groups * ncols;
+      final_jobs.parts[j] = first.dst[j];
+    }
   }
-  if (scratch == nullptr) return hipErrorInvalidValue;
-  const int g = group_size(nparts), groups = (nparts + g - 1) / g;
-  hipLaunchKernelGGL(colsum_parts_kernel, dim3(gx, groups), block, 0, stream, parts, nparts, g, ncols, scratch, row_len,
-                     dst_ld, false);
-  hipLaunchKernelGGL(colsum_parts_kernel, dim3(gx, 1), block, 0, stream, (const float*)scratch, groups, groups, ncols,
-                     dst, row_len, dst_ld, true);
+  if (groups > 1) {
+    if (scratch == nullptr) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(colsum_parts_kernel, dim3(gx, groups, njobs), block, 0, stream, first, nparts, kGroup, ncols,
+                       row_len, dst_ld, false);
+  }
+  const int n2 = groups == 1 ? nparts : groups;
+  hipLaunchKernelGGL(colsum_parts_kernel, dim3(gx, 1, njobs), block, 0, stream, final_jobs, n2, n2, ncols, row_len,
+                     dst_ld, true);
   return hipGetLastError();
+}
+
+hipError_t launch_colsum_reduce(const float* parts, int nparts, long ncols, float* dst, float* scratch,
+                                hipStream_t stream, int row_len, long dst_ld) {
+  return launch_colsum_reduce_multi(&parts, &dst, 1, nparts, ncols, scratch, stream, row_len, dst_ld);
 }
 
 hipError_t launch_embedding_bwd_sorted(const float* dx, const int64_t* sorted_ids, const int64_t* order, float* dwte,

@@ -199,6 +199,11 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const bf16_raw* __r
   }
 }
 
+// x of lane l ^ 1 (DPP quad_perm [1,0,3,2]: one VALU op, no LDS round trip)
+__device__ __forceinline__ float swap_pair(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));
+}
+
 // K^T image [64 d][256 keys]: 512-byte rows, 16-byte chunk index XOR-swizzled by (d & 15) so the
 // 16 rows a ds_read_b128 lane group touches land on 16 distinct chunks (all 64 banks)
 __device__ __forceinline__ int kt_off(int d, int key) { return d * kKvBlk + ((((key >> 3) ^ (d & 15))) << 3) + (key & 7); }
@@ -402,6 +407,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   };
 
   BWD_PROBE(0);
+#ifdef LLMT_BWD_SETPRIO
+  if (wave >= kBwdWaves / 2) __builtin_amdgcn_s_setprio(1);  // A/B: static priority for the younger half
+#endif
   load_tile(kblk0);
   store_tile(0);
   __syncthreads();
@@ -428,19 +436,32 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
       const int i = lane & 15, g = lane >> 4;
       f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
       typedef short short8v __attribute__((ext_vector_type(8)));
-#pragma unroll
-      for (int ks = 0; ks < kKvBlk / 32; ++ks) {
+      // software pipeline: the operands of step ks + 3 are read while step ks's MFMAs run (12 LDS
+      // reads in flight, inside lgkmcnt's 15).  The compiler's own schedule read one pair ahead
+      // and waited on LDS latency before every MFMA (~2.2k cycles for 256 cycles of MFMA);
+      // hoisting all 8 steps' reads spilled (address registers: the K^T swizzle makes every step's
+      // offset distinct).
+      constexpr int kSteps = kKvBlk / 32, kAhead = 3;
+      bf16x8 av[kSteps], b0[kSteps], b1[kSteps];
+      auto read_step = [&](int ks) {
         const int krow = 32 * ks + 8 * g + (i >> 2);
         const int qcol = 16 * qt_dq + 4 * (i & 3);
         const short4v a_lo = tr_read(dsimg, krow, qcol);
         const short4v a_hi = tr_read(dsimg, krow + 4, qcol);
-        const short8v av = {a_lo[0], a_lo[1], a_lo[2], a_lo[3], a_hi[0], a_hi[1], a_hi[2], a_hi[3]};
+        const short8v a8 = {a_lo[0], a_lo[1], a_lo[2], a_lo[3], a_hi[0], a_hi[1], a_hi[2], a_hi[3]};
+        av[ks] = __builtin_bit_cast(bf16x8, a8);
         const int kc = 32 * ks + 8 * g;  // first of this lane's 8 keys
-        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(&kt_lds[kt_off(32 * dp_dq + i, kc)]);
-        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(&kt_lds[kt_off(32 * dp_dq + 16 + i, kc)]);
-        const bf16x8 a = __builtin_bit_cast(bf16x8, av);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b0, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b1, acc1, 0, 0, 0);
+        b0[ks] = *reinterpret_cast<const bf16x8*>(&kt_lds[kt_off(32 * dp_dq + i, kc)]);
+        b1[ks] = *reinterpret_cast<const bf16x8*>(&kt_lds[kt_off(32 * dp_dq + 16 + i, kc)]);
+      };
+#pragma unroll
+      for (int ks = 0; ks < kAhead; ++ks) read_step(ks);
+#pragma unroll
+      for (int ks = 0; ks < kSteps; ++ks) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (ks + kAhead < kSteps) read_step(ks + kAhead);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[ks], b0[ks], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[ks], b1[ks], acc1, 0, 0, 0);
       }
       // this key block's dQ contribution -> its own bf16 partial plane (plain stores; the planes
       // are the largest traffic of the backward: bf16 halves the bytes written here and read by
@@ -453,8 +474,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
       for (int j = 0; j < 2; ++j) {
         const int r = p ? 2 + j : j;  // the row this lane stores
         const int qq = q0 + 16 * qt_dq + 4 * g + r;
-        const float s0 = __shfl_xor(p ? acc0[j] : acc0[2 + j], 1, 64);
-        const float s1 = __shfl_xor(p ? acc1[j] : acc1[2 + j], 1, 64);
+        const float s0 = swap_pair(p ? acc0[j] : acc0[2 + j]);
+        const float s1 = swap_pair(p ? acc1[j] : acc1[2 + j]);
         const float o0 = p ? acc0[2 + j] : acc0[j], o1 = p ? acc1[2 + j] : acc1[j];
         const uint32_t w0 = (uint32_t)f2bf((p ? s0 : o0) * scale) | ((uint32_t)f2bf((p ? o0 : s0) * scale) << 16);
         const uint32_t w1 = (uint32_t)f2bf((p ? s1 : o1) * scale) | ((uint32_t)f2bf((p ? o1 : s1) * scale) << 16);

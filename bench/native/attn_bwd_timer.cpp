@@ -103,8 +103,10 @@ int main(int argc, char** argv) {
                 (r1 - r0) / 100.0, cyc / real * 0.1, real / (double)(r1 - r0));
     for (int kb = 0; kb < nkb; ++kb) std::printf("  kb=%d mean WG duration %.0f cycles\n", kb, dur[kb] / (B * H));
     for (int kb = 0; kb < nkb; ++kb)
-      for (int w = 0; w < 8; w += 7) {
+      for (int w = 0; w < 8; ++w) {
+        if (w != 0 && w != 3 && w != 7) continue;
         const unsigned long long* e = &p[((size_t)kb * 8 + w) * nev];
+        if (e[0] == 0) continue;
         std::printf("probe kb=%d w=%d total=%llu prologue=%llu tiles(phaseA/stage+barrier/dQ):", kb, w, e[63] - e[0],
                     e[1] - e[0]);
         unsigned long long prev = e[1];

@@ -47,7 +47,7 @@ __device__ unsigned long long* g_attn_bwd_probe = nullptr;
   do {                                                                                                   \
     if (g_attn_bwd_probe != nullptr && (threadIdx.x & 63) == 0) {                                        \
       const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                        \
-      if (blockIdx.x == 0 && (ev) < 64) g_attn_bwd_probe[((long)kb * kBwdWaves + wave) * 64 + (ev)] = t_; \
+      if (bh == 0 && (ev) < 64) g_attn_bwd_probe[((long)kb * kBwdWaves + wave) * 64 + (ev)] = t_;         \
       if (threadIdx.x == 0 && ((ev) == 0 || (ev) == 63)) {                                               \
         unsigned long long* g_ = g_attn_bwd_probe + (long)nkb * kBwdWaves * 64 + 4 * ((long)bh * nkb + kb); \
         g_[(ev) == 63] = t_;                                                                             \
@@ -228,8 +228,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int half = lane >> 5, col = lane & 31;
-  const int bh = blockIdx.x;                 // all key blocks of one (b, h) share an XCD
-  const int kb = (int)blockIdx.y;            // ... and the heaviest key blocks (most query tiles) go first
+  // grid (B*H, nkb): chunked heaviest-first dispatch (attention_common.h chunked_dispatch); key
+  // block 0 sees the most query tiles
+  int bh, kb;
+  chunked_dispatch(bh, kb);
   const int b = bh / H, h = bh - b * H;
   const int hd = SMALLHD ? hd_arg : kHD;  // head dim in memory; tiles and fragments stay 64 wide
   const long row_stride = 3L * H * hd;
@@ -566,8 +568,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd4_kernel(const bf16_raw* __res
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int half = lane >> 5, col = lane & 31;
-  const int bh = blockIdx.x;
-  const int kb = (int)blockIdx.y;
+  int bh, kb;
+  chunked_dispatch(bh, kb);
   const int b = bh / H, h = bh - b * H;
   const int hd = SMALLHD ? hd_arg : kHD;
   const long row_stride = 3L * H * hd;

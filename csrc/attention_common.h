@@ -18,6 +18,26 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) short4v lds_short4;
 
+// Dispatch order of a (B*H) x nblk attention grid (x fastest): (b, h) pairs in chunks of
+// kDispatchChunk; inside a chunk every pair's heaviest block first, then the next-heaviest, ...
+// Heaviest-first keeps the causal tail short (a grid that ends on heavy blocks left ~40% of the
+// slots idle); the chunk keeps all blocks of a pair close in time, so its K/V (forward) or Q/dO
+// (backward) are re-read from L2 / Infinity Cache instead of HBM once the whole qkv no longer fits
+// there (B=128: 604 MB).  With chunk and pair counts multiples of 8, every block of a pair runs on
+// one XCD.  Returns (pair, heaviness rank 0 = heaviest).
+constexpr int kDispatchChunk = 64;
+__device__ __forceinline__ void chunked_dispatch(int& pair, int& rank) {
+  const int npairs = gridDim.x, nblk = gridDim.y;
+  const long L = blockIdx.x + (long)gridDim.x * blockIdx.y;
+  const long per_chunk = (long)kDispatchChunk * nblk;
+  const int chunk = (int)(L / per_chunk);
+  const int c0 = chunk * kDispatchChunk;
+  const int cn = min(kDispatchChunk, npairs - c0);
+  const int r = (int)(L - chunk * per_chunk);
+  rank = r / cn;
+  pair = c0 + (r - rank * cn);
+}
+
 // LDS image of a [rows][64] bf16 tile: 128-byte rows of eight 16-byte chunks, chunk index
 // XOR-swizzled by g((row >> 1) & 7) with g(k) = ((k & 1) << 2) | (k >> 1).
 //  * row reads (ds_read_b128; 16 lanes = 16 distinct rows mod 16, one chunk): slot

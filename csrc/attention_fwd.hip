@@ -49,7 +49,7 @@ __device__ unsigned long long* g_attn_probe = nullptr;  // null: no stamps
   do {                                                                                                   \
     if (g_attn_probe != nullptr && (threadIdx.x & 63) == 0) {                                            \
       const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                        \
-      if (blockIdx.x == 0 && (ev) < 64)                                                                  \
+      if (bh == 0 && (ev) < 64)                                                                          \
         g_attn_probe[((long)qb * kFwdWaves + (threadIdx.x >> 6)) * 64 + (ev)] = t_;                      \
       if (threadIdx.x == 0 && ((ev) == 0 || (ev) == 63)) {                                               \
         unsigned long long* g_ = g_attn_probe + (long)nqb * kFwdWaves * 64 + 4 * ((long)bh * nqb + qb);  \
@@ -80,13 +80,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
   // wave-uniform, so hipcc emits scalar branches instead of per-lane exec-mask control flow
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int half = lane >> 5, col = lane & 31;
-  // grid (B*H, nqb), x fastest: dispatch runs through ALL (b, h) of the heaviest (last) query
-  // block first, so the grid ends on the lightest blocks instead of a tail of heavy ones (with
-  // (b, h) outermost the last-dispatched heavy blocks left ~40% of the workgroup slots idle at the
-  // end: 315 of 512 resident on average, bench/native/attn_fwd_timer probe; 0.140 -> 0.104 ms at
-  // B=32).  All blocks of one (b, h) land on one XCD (B*H a multiple of 8), sharing K/V in L2.
-  const int qb = nqb - 1 - (int)blockIdx.y;
-  const int bh = blockIdx.x;
+  // grid (B*H, nqb): chunked heaviest-first dispatch (attention_common.h chunked_dispatch); the
+  // last query block is the heaviest.  (With (b, h) outermost the last-dispatched heavy blocks left
+  // ~40% of the workgroup slots idle at the end: 315 of 512 resident on average,
+  // bench/native/attn_fwd_timer probe.)
+  int bh, qrank;
+  chunked_dispatch(bh, qrank);
+  const int qb = nqb - 1 - qrank;
   const int b = bh / H, h = bh - b * H;
   const int hd = SMALLHD ? hd_arg : kHD;  // head dim in memory; tiles stay 64 wide
   const long row_stride = 3L * H * hd;   // elements between consecutive tokens in qkv

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -29,11 +30,15 @@ void attn_bwd_probe_set(unsigned long long* buf);
   } while (0)
 
 int main(int argc, char** argv) {
-  const int B = argc > 1 ? std::atoi(argv[1]) : 32, T = 1024, H = 12, D = 64;
+  // argv: B [label] [head_dim: 64 or 128; H keeps d_model = 768]
+  const int D = argc > 3 ? std::atoi(argv[3]) : 64;
+  const int B = argc > 1 ? std::atoi(argv[1]) : 32, T = 1024, H = 768 / D;
   llmt::AttnDims dims;
   dims.B = B;
   dims.T = T;
   dims.H = H;
+  dims.hd = D;
+  dims.scale = 1.0f / std::sqrt((float)D);
   const size_t nqkv = (size_t)B * T * 3 * H * D, nout = (size_t)B * T * H * D, nrow = (size_t)B * H * T;
   std::vector<unsigned short> h(nqkv);
   unsigned s = 12345;
@@ -52,7 +57,7 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&out, nout * 2));
   CHECK(hipMalloc(&lse, nrow * 4));
   CHECK(hipMalloc(&delta, nrow * 4));
-  CHECK(hipMalloc(&dq, llmt::attn_bwd_workspace_floats(B, T, H) * 4));
+  CHECK(hipMalloc(&dq, llmt::attn_bwd_workspace_floats(B, T, H, D) * 4));
   CHECK(hipMemcpy(qkv, h.data(), nqkv * 2, hipMemcpyHostToDevice));
   CHECK(hipMemcpy(dout, h.data(), nout * 2, hipMemcpyHostToDevice));
   CHECK(hipMemcpy(out, h.data() + nout, nout * 2, hipMemcpyHostToDevice));
@@ -119,7 +124,7 @@ int main(int argc, char** argv) {
   }
 #endif
   const double flops = 2.5 * 4.0 * B * H * (double)T * T * D / 2;
-  std::printf("{\"kernel\": \"attn_bwd\", \"variant\": \"%s\", \"B\": %d, \"ms\": %.4f, \"TFLOPs\": %.1f}\n",
-              argc > 2 ? argv[2] : "?", B, ms[ms.size() / 2], flops / ms[ms.size() / 2] / 1e9);
+  std::printf("{\"kernel\": \"attn_bwd\", \"variant\": \"%s\", \"B\": %d, \"hd\": %d, \"ms\": %.4f, \"TFLOPs\": %.1f}\n",
+              argc > 2 ? argv[2] : "?", B, D, ms[ms.size() / 2], flops / ms[ms.size() / 2] / 1e9);
   return 0;
 }

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -26,11 +27,15 @@ void attn_probe_set(unsigned long long* buf);
   } while (0)
 
 int main(int argc, char** argv) {
-  const int B = argc > 1 ? std::atoi(argv[1]) : 32, T = 1024, H = 12, D = 64;
+  // argv: B [label] [head_dim: 64 or 128; H keeps d_model = 768]
+  const int D = argc > 3 ? std::atoi(argv[3]) : 64;
+  const int B = argc > 1 ? std::atoi(argv[1]) : 32, T = 1024, H = 768 / D;
   llmt::AttnDims dims;
   dims.B = B;
   dims.T = T;
   dims.H = H;
+  dims.hd = D;
+  dims.scale = 1.0f / std::sqrt((float)D);
   const size_t nqkv = (size_t)B * T * 3 * H * D, nout = (size_t)B * T * H * D, nrow = (size_t)B * H * T;
   std::vector<unsigned short> h(nqkv);
   unsigned s = 12345;
@@ -110,7 +115,7 @@ int main(int argc, char** argv) {
   }
 #endif
   const double flops = 4.0 * B * H * (double)T * T * D / 2;
-  std::printf("{\"kernel\": \"attn_fwd\", \"variant\": \"%s\", \"B\": %d, \"ms\": %.4f, \"TFLOPs\": %.1f}\n",
-              argc > 2 ? argv[2] : "?", B, ms[ms.size() / 2], flops / ms[ms.size() / 2] / 1e9);
+  std::printf("{\"kernel\": \"attn_fwd\", \"variant\": \"%s\", \"B\": %d, \"hd\": %d, \"ms\": %.4f, \"TFLOPs\": %.1f}\n",
+              argc > 2 ? argv[2] : "?", B, D, ms[ms.size() / 2], flops / ms[ms.size() / 2] / 1e9);
   return 0;
 }

@@ -71,22 +71,24 @@ constexpr int kQTile = 64;  // query rows per sweep step (two 32-row MFMA tiles)
 // workgroup stores its hd partial sums to vparts[b * gridDim.x + blockIdx.x][h * hd + d] (no
 // atomics: 512+ workgroups per head would serialise on the same 64 addresses);
 // launch_colsum_reduce sums them in a fixed order.
+// NH = 64-wide halves of the head dim (2: hd = 128): 8 * NH lanes per row, 32 / NH rows per sweep.
 constexpr int kDeltaRows = 256;
-template <bool SMALLHD>
+template <bool SMALLHD, int NH = 1>
 __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restrict__ dout,
                                                          const bf16_raw* __restrict__ out,
                                                          float* __restrict__ delta, float* __restrict__ vparts,
                                                          int T, int H, int hd_arg) {
-  const int hd = SMALLHD ? hd_arg : kHD;
-  __shared__ float red[4][kHD];
+  constexpr int kLpr = 8 * NH, kRps = 256 / kLpr;  // lanes per row, rows per sweep
+  const int hd = SMALLHD ? hd_arg : kHD * NH;
+  __shared__ float red[4][kHD * NH];
   const int bh = blockIdx.y;
   const int b = bh / H, h = bh - b * H;
-  const int rl = threadIdx.x >> 3, sub = threadIdx.x & 7;
-  constexpr int kSweeps = kDeltaRows / 32;
+  const int rl = threadIdx.x / kLpr, sub = threadIdx.x % kLpr;
+  constexpr int kSweeps = kDeltaRows / kRps;
   ushort8_t dv[kSweeps], ov[kSweeps];
 #pragma unroll
   for (int it = 0; it < kSweeps; ++it) {
-    const int t = blockIdx.x * kDeltaRows + 32 * it + rl;
+    const int t = blockIdx.x * kDeltaRows + kRps * it + rl;
     dv[it] = ushort8_t{0, 0, 0, 0, 0, 0, 0, 0};
     ov[it] = dv[it];
     if (t < T && 8 * sub < hd) {
@@ -107,22 +109,19 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
       acc += a[i] * o[i];
       csum[i] += a[i];  // rows past T loaded as zeros
     }
-    acc += __shfl_xor(acc, 1, 64);
-    acc += __shfl_xor(acc, 2, 64);
-    acc += __shfl_xor(acc, 4, 64);
-    const int t = blockIdx.x * kDeltaRows + 32 * it + rl;
+#pragma unroll
+    for (int off = 1; off < kLpr; off <<= 1) acc += __shfl_xor(acc, off, 64);
+    const int t = blockIdx.x * kDeltaRows + kRps * it + rl;
     if (t < T && sub == 0) delta[(long)bh * T + t] = acc;
   }
   if (vparts == nullptr) return;  // uniform: kernel argument
-  // column sums: over the wave's 8 rows with shuffles (lanes sharing `sub`), then the 4 waves
+  // column sums: over the wave's rows with shuffles (lanes sharing `sub`), then the 4 waves
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    csum[i] += __shfl_xor(csum[i], 8, 64);
-    csum[i] += __shfl_xor(csum[i], 16, 64);
-    csum[i] += __shfl_xor(csum[i], 32, 64);
-  }
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int off = kLpr; off < 64; off <<= 1) csum[i] += __shfl_xor(csum[i], off, 64);
   const int wv = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) < 8) {
+  if ((threadIdx.x & 63) < kLpr) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) red[wv][8 * sub + i] = csum[i];
   }
@@ -142,19 +141,20 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_raw* __restr
 // gradient (column sums of dQ) leaves the workgroup as one partial row,
 // qparts[b * gridDim.y + tile][h * hd + d] (fixed-order reduce afterwards, no atomics).
 constexpr int kDqRows = 64;
-template <bool SMALLHD>
+template <bool SMALLHD, int NH = 1>
 __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const bf16_raw* __restrict__ part, bf16_raw* __restrict__ dqkv,
                                                              float* __restrict__ qparts, int T, int H, int hd_arg,
-                                                             int nkb, long plane) {
-  const int hd = SMALLHD ? hd_arg : kHD;
-  __shared__ float red[4][kHD];
+                                                             int nkb, long plane, int kvblk) {
+  constexpr int kLpr = 8 * NH, kRps = 256 / kLpr, kW = kHD * NH;  // lanes per row, rows per sweep, width
+  const int hd = SMALLHD ? hd_arg : kW;
+  __shared__ float red[4][kW];
   const int bh = blockIdx.x;
   const int b = bh / H, h = bh - b * H;
-  const int rl = threadIdx.x >> 3, c = threadIdx.x & 7;
+  const int rl = threadIdx.x / kLpr, c = threadIdx.x % kLpr;
   const int tile = (int)(gridDim.y - 1 - blockIdx.y);  // heavy (late) rows first
-  const int t0 = tile * kDqRows + rl;  // this thread's rows: t0 + 32 * it
-  const int last = min(tile * kDqRows / kKvBlk, nkb - 1);
-  constexpr int kSweeps = kDqRows / 32;
+  const int t0 = tile * kDqRows + rl;  // this thread's rows: t0 + kRps * it
+  const int last = min(tile * kDqRows / kvblk, nkb - 1);
+  constexpr int kSweeps = kDqRows / kRps;
   // key-block planes outermost: each plane step issues all 8 loads of the thread's 8 rows at
   // once (rows past T re-read row T - 1, which every plane up to `last` holds; result unused)
   float f[kSweeps][8];
@@ -165,9 +165,9 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const bf16_raw* __r
   for (int kb = 0; kb <= last; ++kb) {
 #pragma unroll
     for (int it = 0; it < kSweeps; ++it) {
-      const int t = min(t0 + 32 * it, T - 1);
+      const int t = min(t0 + kRps * it, T - 1);
       float x[8];
-      unpack8(*reinterpret_cast<const ushort8_t*>(part + kb * plane + ((long)bh * T + t) * kHD + 8 * c), x);
+      unpack8(*reinterpret_cast<const ushort8_t*>(part + kb * plane + ((long)bh * T + t) * kW + 8 * c), x);
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[it][j] += x[j];
     }
@@ -175,8 +175,8 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const bf16_raw* __r
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int it = 0; it < kSweeps; ++it) {
-    const int t = t0 + 32 * it;
-    if (t < T && 8 * c < hd) {  // the partial planes are 64 wide; dims >= hd are zero
+    const int t = t0 + kRps * it;
+    if (t < T && 8 * c < hd) {  // the partial planes are kW wide; dims >= hd are zero
       *reinterpret_cast<ushort8_t*>(dqkv + ((long)b * T + t) * 3L * H * hd + (long)h * hd + 8 * c) = pack8(f[it]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) csum[j] += f[it][j];
@@ -184,13 +184,11 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const bf16_raw* __r
   }
   if (qparts == nullptr) return;  // uniform: kernel argument
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    csum[j] += __shfl_xor(csum[j], 8, 64);
-    csum[j] += __shfl_xor(csum[j], 16, 64);
-    csum[j] += __shfl_xor(csum[j], 32, 64);
-  }
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int off = kLpr; off < 64; off <<= 1) csum[j] += __shfl_xor(csum[j], off, 64);
   const int wv = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) < 8) {
+  if ((threadIdx.x & 63) < kLpr) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[wv][8 * c + j] = csum[j];
   }
@@ -871,11 +869,308 @@ __global__ __launch_bounds__(256, 1) void attn_bwd4_kernel(const bf16_raw* __res
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Head dim 128: 4 waves (one per SIMD, 512 registers per lane) x 32 keys = a 128-key block.  The
+// 8-wave kernel's per-wave state doubles at hd = 128 (dK^T / dV^T 128 registers, K/V fragments 64)
+// and no longer fits two waves per SIMD; here each wave keeps dK^T / dV^T of its 32 keys over the
+// full 128 dims, its K/V fragments, and the B operand of dQ = dS K for its 32 dQ columns over the
+// block's 128 keys (read once from a K^T image).  Q/dO tiles are [64][128], kept as two [64][64]
+// swizzled LDS images each; dS^T crosses LDS as in the other kernels.  Same contract, masks,
+// dropout; dQ partial planes are 128 wide, one per 128-key block.
+constexpr int kKv128 = 128;
+__device__ __forceinline__ int kt128_off(int d, int key) {
+  return d * kKv128 + ((((key >> 3) ^ (d & 15))) << 3) + (key & 7);
+}
+
+template <bool DROPOUT, bool KMASK>
+__global__ __launch_bounds__(256, 1) void attn_bwd128_kernel(const bf16_raw* __restrict__ qkv,
+                                                             const bf16_raw* __restrict__ dout,
+                                                             const float* __restrict__ lse,
+                                                             const float* __restrict__ delta,
+                                                             bf16_raw* __restrict__ dqkv,
+                                                             float* __restrict__ dq_part, float* __restrict__ vparts,
+                                                             int T, int H, int nkb, DropoutArgs dr,
+                                                             const uint8_t* __restrict__ key_valid) {
+  constexpr int hd = 2 * kHD;
+  __shared__ __attribute__((aligned(16))) bf16_raw qd_lds[2][2][2][kQTile * kHD];  // [buf][Q|dO][half] 64 KB
+  __shared__ __attribute__((aligned(16))) bf16_raw ds_lds[2][kKv128 * kQTile];     // [buf][key][q] 32 KB
+  __shared__ __attribute__((aligned(16))) float rowc_lds[2][2 * kQTile];
+  __shared__ float bias_red[4][hd];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int half = lane >> 5, col = lane & 31;
+  int bh, kb;
+  chunked_dispatch(bh, kb);
+  const int b = bh / H, h = bh - b * H;
+  const long row_stride = 3L * H * hd;
+  const bf16_raw* base = qkv + (long)b * T * row_stride + (long)h * hd;
+  const bf16_raw* dobase = dout + (long)b * T * H * hd + (long)h * hd;
+  const long out_stride = (long)H * hd;
+  const float* lse_bh = lse + ((long)b * H + h) * T;
+  const float* delta_bh = delta + ((long)b * H + h) * T;
+  const __amdgpu_buffer_rsrc_t r_q = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0,
+                                                                        (int)((T - 1) * row_stride + hd) * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r_kv = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0,
+                                                                         (int)((T - 1) * row_stride + 3 * hd * H) * 2,
+                                                                         0x00020000);
+  const __amdgpu_buffer_rsrc_t r_do = __builtin_amdgcn_make_buffer_rsrc((void*)dobase, (short)0,
+                                                                         (int)((T - 1) * out_stride + hd) * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r_lse = __builtin_amdgcn_make_buffer_rsrc((void*)lse_bh, (short)0, T * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r_del = __builtin_amdgcn_make_buffer_rsrc((void*)delta_bh, (short)0, T * 4, 0x00020000);
+
+  const uint32_t pseed = DROPOUT ? mix32(dr.seed + (uint32_t)bh * 0x9E3779B9u) : 0u;
+  const int kblk0 = kb * kKv128;
+  const int kw0 = kblk0 + 32 * wave;
+  const int key = kw0 + col;
+  constexpr float scale = 0.08838834764831845f;  // 1 / sqrt(128)
+  const float c = scale * 1.4426950408889634f;
+  const bool kvalid = !KMASK || (key < T && key_valid[(long)b * T + key] != 0);
+
+  bf16x8 kf[8], vf[8];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    const int off = (int)(key * row_stride + 16 * kk + 8 * half) * 2;
+    kf[kk] = __builtin_bit_cast(bf16x8, buf_load16(r_kv, off + hd * H * 2));
+    vf[kk] = __builtin_bit_cast(bf16x8, buf_load16(r_kv, off + 2 * hd * H * 2));
+  }
+  // dQ B operand (16x16x32, k = key, n = d): lane l holds K[32 ks + 8 (l >> 4) + 0..7][32 w + 16 dn + (l & 15)],
+  // read once through a K^T image [128 d][128 keys] laid over both dS buffers
+  bf16x8 kq[kKv128 / 32][2];
+  {
+    bf16_raw* kt_img = ds_lds[0];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const ushort8_t kv = __builtin_bit_cast(ushort8_t, kf[kk]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) kt_img[kt128_off(16 * kk + 8 * half + e, 32 * wave + col)] = kv[e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < kKv128 / 32; ++ks)
+#pragma unroll
+      for (int dn = 0; dn < 2; ++dn)
+        kq[ks][dn] = *reinterpret_cast<const bf16x8*>(&kt_img[kt128_off(32 * wave + 16 * dn + (lane & 15), 32 * ks + 8 * (lane >> 4))]);
+    __syncthreads();  // every wave's reads of the image are done before the first dS write
+  }
+
+  // register staging of one 64-row Q/dO tile (+ row constants): 4 Q + 4 dO chunks per thread
+  ushort8_t stg[8];
+  float stc = 0.f;
+  auto load_tile = [&](int q0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int cidx = threadIdx.x + 256 * (i & 3);
+      const int r = cidx >> 4, ch = cidx & 15;
+      const int qrow = q0 + r;
+      stg[i] = i < 4 ? buf_load16(r_q, (int)(qrow * row_stride + ch * 8) * 2)
+                     : buf_load16(r_do, (int)(qrow * out_stride + ch * 8) * 2);
+    }
+    if (threadIdx.x < 2 * kQTile) {
+      const int qq = q0 + (threadIdx.x & (kQTile - 1));
+      stc = threadIdx.x < kQTile ? buf_load_f32(r_lse, qq * 4) : buf_load_f32(r_del, qq * 4);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int cidx = threadIdx.x + 256 * (i & 3);
+      const int r = cidx >> 4, ch = cidx & 15;
+      *reinterpret_cast<ushort8_t*>(&qd_lds[buf][i >> 2][ch >> 3][tile_chunk_off(r, ch & 7)]) = stg[i];
+    }
+    if (threadIdx.x < 2 * kQTile) rowc_lds[buf][threadIdx.x] = threadIdx.x < kQTile ? stc * 1.4426950408889634f : stc;
+  };
+
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    dk[dt] = 0.f;
+    dv[dt] = 0.f;
+  }
+
+  auto phase_a = [&](bool full, int q0, int buf, bf16_raw* dsimg) {
+    const float* rowc = rowc_lds[buf];
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      const int qb0 = q0 + 32 * qs;
+      const bool active = full || (kw0 <= qb0 + 31 && kw0 < T && qb0 < T);
+      f32x16 ds;
+      if (active) {
+        f32x16 p = 0.f, dp = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+          const bf16x8 qa = lds_row_read(qd_lds[buf][0][kk >> 2], 32 * qs + col, 2 * (kk & 3) + half);
+          const bf16x8 da = lds_row_read(qd_lds[buf][1][kk >> 2], 32 * qs + col, 2 * (kk & 3) + half);
+          p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[kk], p, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[kk], dp, 0, 0, 0);
+        }
+        float ddv[16];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const f32x4 l2 = *reinterpret_cast<const f32x4*>(&rowc[32 * qs + 8 * rr + 4 * half]);
+          const f32x4 dd = *reinterpret_cast<const f32x4*>(&rowc[kQTile + 32 * qs + 8 * rr + 4 * half]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            p[4 * rr + i] = __builtin_amdgcn_exp2f(fmaf(p[4 * rr + i], c, -l2[i]));
+            if (DROPOUT) ddv[4 * rr + i] = dd[i];
+            else dp[4 * rr + i] -= dd[i];
+          }
+        }
+        if (KMASK && !kvalid) p = 0.f;
+        if (!full && ((kw0 + 31 > qb0) || (kw0 + 32 > T) || (qb0 + 32 > T))) {
+          const int lo = key - qb0 - 4 * half, hi = T - 1 - qb0 - 4 * half;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int roff = (r & 3) + 8 * (r >> 2);
+            p[r] = (roff < lo || roff > hi) ? 0.f : p[r];
+          }
+        }
+        if (DROPOUT) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const uint32_t qq = (uint32_t)(qb0 + 4 * half + (r & 3) + 8 * (r >> 2));
+            const bool kp = drop_keep(pseed, dr.thr, qq * (uint32_t)T + (uint32_t)key);
+            ds[r] = p[r] * ((kp ? dp[r] * dr.scale : 0.f) - ddv[r]);
+            p[r] = kp ? p[r] * dr.scale : 0.f;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) ds[r] = p[r] * dp[r];
+        }
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const bf16x8 pb = pack_acc8(p, st);
+          const bf16x8 sb = pack_acc8(ds, st);
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) {
+            const int rb = 32 * qs + 16 * st + 4 * half;
+            const bf16x8 doa = lds_tr_read_operand(qd_lds[buf][1][dt >> 1], rb, (dt & 1) * 32, lane);
+            dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(doa, pb, dv[dt], 0, 0, 0);
+            const bf16x8 qa = lds_tr_read_operand(qd_lds[buf][0][dt >> 1], rb, (dt & 1) * 32, lane);
+            dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, sb, dk[dt], 0, 0, 0);
+          }
+        }
+      } else {
+        ds = 0.f;
+      }
+      const int kl = 32 * wave + col;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        ushort4_t v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = f2bf(ds[4 * g + i]);
+        *reinterpret_cast<ushort4_t*>(&dsimg[tile_elem_off(kl, 32 * qs + 8 * g + 4 * half)]) = v;
+      }
+    }
+  };
+
+  load_tile(kblk0);
+  store_tile(0);
+  __syncthreads();
+
+  int it = 0;
+  for (int q0 = kblk0; q0 < T; q0 += kQTile, ++it) {
+    const int cur = it & 1;
+    const bool more = q0 + kQTile < T;
+    if (more) load_tile(q0 + kQTile);
+    phase_a(q0 >= kblk0 + kKv128 && q0 + kQTile <= T, q0, cur, ds_lds[cur]);
+    if (more) store_tile(cur ^ 1);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+    // ---- dQ[q0 + 16 qt + .., 32 w + 16 dn + ..] = dS K over the block's 128 keys (16x16x32) ----
+    {
+      const int i = lane & 15, g = lane >> 4;
+      const bf16_raw* dsimg = ds_lds[cur];
+      f32x4 acc[4][2];
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+        for (int dn = 0; dn < 2; ++dn) acc[qt][dn] = f32x4{0.f, 0.f, 0.f, 0.f};
+      typedef short short8v __attribute__((ext_vector_type(8)));
+#pragma unroll
+      for (int ks = 0; ks < kKv128 / 32; ++ks) {
+        const int krow = 32 * ks + 8 * g + (i >> 2);
+#pragma unroll
+        for (int qt = 0; qt < 4; ++qt) {
+          const int qcol = 16 * qt + 4 * (i & 3);
+          const short4v lo = tr_read(dsimg, krow, qcol);
+          const short4v hi = tr_read(dsimg, krow + 4, qcol);
+          const short8v a8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          const bf16x8 a = __builtin_bit_cast(bf16x8, a8);
+#pragma unroll
+          for (int dn = 0; dn < 2; ++dn)
+            acc[qt][dn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, kq[ks][dn], acc[qt][dn], 0, 0, 0);
+        }
+      }
+      const int p = i & 1;
+      bf16_raw* plane = reinterpret_cast<bf16_raw*>(dq_part) + ((long)kb * gridDim.x + bh) * T * hd;
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int r = p ? 2 + jj : jj;
+          const int qq = q0 + 16 * qt + 4 * g + r;
+#pragma unroll
+          for (int dn = 0; dn < 2; ++dn) {
+            const float sw = swap_pair(p ? acc[qt][dn][jj] : acc[qt][dn][2 + jj]);
+            const float own = p ? acc[qt][dn][2 + jj] : acc[qt][dn][jj];
+            const uint32_t w = (uint32_t)f2bf((p ? sw : own) * scale) | ((uint32_t)f2bf((p ? own : sw) * scale) << 16);
+            if (qq < T) *reinterpret_cast<uint32_t*>(plane + (long)qq * hd + 32 * wave + 16 * dn + (i & ~1)) = w;
+          }
+        }
+      }
+    }
+  }
+
+  if (key < T) {
+    bf16_raw* dst = dqkv + ((long)b * T + key) * row_stride + (long)h * hd;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        ushort4_t kv, vv;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          kv[i] = f2bf(dk[dt][4 * g + i] * scale);
+          vv[i] = f2bf(dv[dt][4 * g + i]);
+        }
+        const int d = dt * 32 + 8 * g + 4 * half;
+        *reinterpret_cast<ushort4_t*>(dst + hd * H + d) = kv;
+        *reinterpret_cast<ushort4_t*>(dst + 2 * hd * H + d) = vv;
+      }
+    }
+  }
+  if (!DROPOUT || vparts == nullptr) return;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float vv = dv[dt][r];
+#pragma unroll
+      for (int off = 1; off < 32; off <<= 1) vv += __shfl_xor(vv, off, 64);
+      if (col == 0) bias_red[wave][dt * 32 + 8 * (r >> 2) + 4 * half + (r & 3)] = vv;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < hd) {
+    float acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) acc += bias_red[w][threadIdx.x];
+    vparts[((long)b * nkb + kb) * (H * hd) + h * hd + threadIdx.x] = acc;
+  }
+}
+
 }  // namespace attn
 
-long attn_bwd_workspace_floats(int B, int T, int H) {
-  const long nkb = (T + attn::kKvBlk - 1) / attn::kKvBlk;
-  return (nkb * B * H * (long)T * attn::kHD + 1) / 2;  // bf16 planes
+namespace {
+// key-block size of the backward: 256 (8-wave kernel) for hd <= 64, 128 for hd = 128
+int bwd_kvblk(int hd) { return hd == 2 * attn::kHD ? attn::kKv128 : attn::kKvBlk; }
+int bwd_plane_width(int hd) { return hd == 2 * attn::kHD ? 2 * attn::kHD : attn::kHD; }
+}  // namespace
+
+long attn_bwd_workspace_floats(int B, int T, int H, int hd) {
+  const long nkb = (T + bwd_kvblk(hd) - 1) / bwd_kvblk(hd);
+  return (nkb * B * H * (long)T * bwd_plane_width(hd) + 1) / 2;  // bf16 planes
 }
 
 namespace {
@@ -886,7 +1181,7 @@ struct BiasParts {
   long cols;
 };
 BiasParts bias_parts(int B, int T, int H, int hd) {
-  const int nkb = (T + attn::kKvBlk - 1) / attn::kKvBlk;
+  const int nkb = (T + bwd_kvblk(hd) - 1) / bwd_kvblk(hd);
   const int nv1 = B * ((T + attn::kDeltaRows - 1) / attn::kDeltaRows), nv2 = B * nkb;
   return {nv1 > nv2 ? nv1 : nv2, B * ((T + attn::kDqRows - 1) / attn::kDqRows), (long)H * hd};
 }
@@ -925,7 +1220,9 @@ hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, c
                            float* delta, float* dq_part, float* dbias, float* bias_ws, const AttnDims& d,
                            DropoutArgs dropout, hipStream_t stream, bool delta_ready) {
   const int B = d.B, T = d.T, H = d.H, hd = d.hd;
-  if (B <= 0 || T <= 0 || H <= 0 || T > 65535 || hd <= 0 || hd > attn::kHD || hd % 8 != 0) return hipErrorInvalidValue;
+  const bool hd128 = hd == 2 * attn::kHD;
+  if (B <= 0 || T <= 0 || H <= 0 || T > 65535 || hd <= 0 || (hd > attn::kHD && !hd128) || hd % 8 != 0)
+    return hipErrorInvalidValue;
   if (dbias != nullptr && bias_ws == nullptr) return hipErrorInvalidValue;
   const long rows = (long)B * T * H;
   const BiasParts bp = bias_parts(B, T, H, hd);
@@ -934,11 +1231,15 @@ hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, c
   float* scratch = dbias != nullptr ? bias_ws + (long)(bp.nv + bp.nq) * bp.cols : nullptr;
   const bool v_from_delta = !delta_ready && dropout.thr == 0 && dbias != nullptr;
   const dim3 dgrid((T + attn::kDeltaRows - 1) / attn::kDeltaRows, B * H);
-  const bool small = hd != attn::kHD;
-  if (!delta_ready)
-    hipLaunchKernelGGL(small ? attn::attn_delta_kernel<true> : attn::attn_delta_kernel<false>, dgrid, dim3(256), 0, stream,
-                       (const bf16_raw*)dout, (const bf16_raw*)out, delta, v_from_delta ? vparts : nullptr, T, H, hd);
-  const int nkb = (T + attn::kKvBlk - 1) / attn::kKvBlk;
+  const bool small = hd < attn::kHD;
+  if (!delta_ready) {
+    auto dk = hd128 ? attn::attn_delta_kernel<false, 2>
+                    : (small ? attn::attn_delta_kernel<true> : attn::attn_delta_kernel<false>);
+    hipLaunchKernelGGL(dk, dgrid, dim3(256), 0, stream, (const bf16_raw*)dout, (const bf16_raw*)out, delta,
+                       v_from_delta ? vparts : nullptr, T, H, hd);
+  }
+  const int kvblk = bwd_kvblk(hd);
+  const int nkb = (T + kvblk - 1) / kvblk;
   const dim3 grid(B * H, nkb);
   const bool drop = dropout.thr != 0, km = d.key_valid != nullptr;
   const int variant = (drop ? 4 : 0) | (km ? 2 : 0) | (small ? 1 : 0);
@@ -946,6 +1247,12 @@ hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, c
   auto g = (const bf16_raw*)dout;
   auto dq = (bf16_raw*)dqkv;
   float* vp = drop ? vparts : nullptr;  // the main kernel forms the V-bias partials only with dropout
+  if (hd128) {
+    auto k = drop ? (km ? attn::attn_bwd128_kernel<true, true> : attn::attn_bwd128_kernel<true, false>)
+                  : (km ? attn::attn_bwd128_kernel<false, true> : attn::attn_bwd128_kernel<false, false>);
+    hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, q, g, lse, delta, dq, dq_part, vp, T, H, nkb, dropout,
+                       d.key_valid);
+  } else {
   switch (variant) {
     case 0: launch_bwd_variant<false, false, false>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
     case 1: launch_bwd_variant<false, false, true>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
@@ -956,9 +1263,12 @@ hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, c
     case 6: launch_bwd_variant<true, true, false>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
     default: launch_bwd_variant<true, true, true>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
   }
+  }
   const dim3 rgrid(B * H, (T + attn::kDqRows - 1) / attn::kDqRows);
-  hipLaunchKernelGGL(small ? attn::attn_dq_reduce_kernel<true> : attn::attn_dq_reduce_kernel<false>, rgrid, dim3(256),
-                     0, stream, (const bf16_raw*)dq_part, dq, qparts, T, H, hd, nkb, rows * (long)attn::kHD);
+  auto rk = hd128 ? attn::attn_dq_reduce_kernel<false, 2>
+                  : (small ? attn::attn_dq_reduce_kernel<true> : attn::attn_dq_reduce_kernel<false>);
+  hipLaunchKernelGGL(rk, rgrid, dim3(256), 0, stream, (const bf16_raw*)dq_part, dq, qparts, T, H, hd, nkb,
+                     rows * (long)bwd_plane_width(hd), kvblk);
   if (dbias != nullptr) {
     // fixed-order sums of the partial rows: Q part, then (unless the out-proj GEMM's epilogue
     // already added it) the V part; the K part of the qkv-bias gradient is exactly zero

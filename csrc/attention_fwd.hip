@@ -68,13 +68,15 @@ constexpr int kFwdWaves = 4;
 constexpr int kQBlk = 32 * kFwdWaves;  // 128 query rows per workgroup
 constexpr int kKBlk = 64;              // keys per LDS tile
 
-template <bool DROPOUT, bool KMASK, bool SMALLHD>
+// NH: 64-wide halves of the head dim (1: hd <= 64; 2: hd = 128, every [64][128] K/V tile kept as two
+// [64][64] LDS images so the swizzle and fragment readers stay the 64-wide ones)
+template <bool DROPOUT, bool KMASK, bool SMALLHD, int NH = 1>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __restrict__ qkv,
                                                           bf16_raw* __restrict__ out,
                                                           float* __restrict__ lse, int T, int H,
                                                           int nqb, DropoutArgs dr, int hd_arg, float c_arg,
                                                           const uint64_t* __restrict__ key_bits) {
-  __shared__ __attribute__((aligned(16))) bf16_raw smem[2][2][kKBlk * kHD];  // [buf][K|V][tile]
+  __shared__ __attribute__((aligned(16))) bf16_raw smem[2][2][NH][kKBlk * kHD];  // [buf][K|V][half][tile]
   const int lane = threadIdx.x & 63;
   // readfirstlane makes the wave index (and every tile/mask decision derived from it) provably
   // wave-uniform, so hipcc emits scalar branches instead of per-lane exec-mask control flow
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
   chunked_dispatch(bh, qrank);
   const int qb = nqb - 1 - qrank;
   const int b = bh / H, h = bh - b * H;
-  const int hd = SMALLHD ? hd_arg : kHD;  // head dim in memory; tiles stay 64 wide
+  const int hd = SMALLHD ? hd_arg : kHD * NH;  // head dim in memory; tiles stay 64 wide
   const long row_stride = 3L * H * hd;   // elements between consecutive tokens in qkv
   const bf16_raw* base = qkv + (long)b * T * row_stride + (long)h * hd;
   // attention-probability dropout: plane seed per (b, h), element index q*T + key
@@ -99,9 +101,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
   const int q_hi = min(q0w + 31, T - 1);     // last valid query row of the wave
 
   // Q fragments (B operand of S^T = K Q^T): lane holds Q[q][16kk + 8*half + 0..7]
-  bf16x8 qf[4];
+  bf16x8 qf[4 * NH];
 #pragma unroll
-  for (int kk = 0; kk < 4; ++kk) {
+  for (int kk = 0; kk < 4 * NH; ++kk) {
     ushort8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
     if (q < T && (!SMALLHD || 16 * kk + 8 * half < hd))
       v = *reinterpret_cast<const ushort8_t*>(base + (long)q * row_stride + 16 * kk + 8 * half);
@@ -116,12 +118,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
   // keys past the sequence read as zeros without branches.
   const __amdgpu_buffer_rsrc_t rkv = __builtin_amdgcn_make_buffer_rsrc(
       (void*)base, (short)0, (int)(((long)T - 1) * row_stride + 3 * hd * H) * 2, 0x00020000);
-  ushort8_t st0[4], st1[4];
-  auto load_tile = [&](ushort8_t(&st)[4], int tile) {
+  constexpr int kCh = 2 * NH;  // 16-byte chunks per thread per K (and per V) tile
+  ushort8_t st0[2 * kCh], st1[2 * kCh];
+  auto load_tile = [&](ushort8_t(&st)[2 * kCh], int tile) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kCh; ++i) {
       const int c = threadIdx.x + 256 * i;
-      const int r = c >> 3, ch = c & 7;
+      const int r = c / (8 * NH), ch = c % (8 * NH);
       // chunks past a small head dim are never read: an offset past the descriptor's record
       // count loads zeros (reading them would run past the last head of the last token, i.e.
       // past the end of the qkv allocation, by (64 - hd) * 2 bytes)
@@ -129,25 +132,25 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
       const int off = live ? (int)(((long)(tile * kKBlk + r) * row_stride + ch * 8 + hd * H) * 2) : kOobOff;
       const int off_v = live ? off + hd * H * 2 : kOobOff;
       st[i] = __builtin_bit_cast(ushort8_t, __builtin_amdgcn_raw_buffer_load_b128(rkv, off, 0, 0));
-      st[2 + i] = __builtin_bit_cast(ushort8_t, __builtin_amdgcn_raw_buffer_load_b128(rkv, off_v, 0, 0));
+      st[kCh + i] = __builtin_bit_cast(ushort8_t, __builtin_amdgcn_raw_buffer_load_b128(rkv, off_v, 0, 0));
     }
   };
-  auto store_tile = [&](const ushort8_t(&st)[4], int buf) {
+  auto store_tile = [&](const ushort8_t(&st)[2 * kCh], int buf) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kCh; ++i) {
       const int c = threadIdx.x + 256 * i;
-      const int r = c >> 3, ch = c & 7;
-      const int off = tile_chunk_off(r, ch);
-      *reinterpret_cast<ushort8_t*>(&smem[buf][0][off]) = st[i];
-      *reinterpret_cast<ushort8_t*>(&smem[buf][1][off]) = st[2 + i];
+      const int r = c / (8 * NH), ch = c % (8 * NH);
+      const int off = tile_chunk_off(r, ch & 7);
+      *reinterpret_cast<ushort8_t*>(&smem[buf][0][ch >> 3][off]) = st[i];
+      *reinterpret_cast<ushort8_t*>(&smem[buf][1][ch >> 3][off]) = st[kCh + i];
     }
   };
 
-  f32x16 o[2];
-  o[0] = 0.f;
-  o[1] = 0.f;
+  f32x16 o[2 * NH];
+#pragma unroll
+  for (int dt = 0; dt < 2 * NH; ++dt) o[dt] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
-  const float c = SMALLHD ? c_arg : 0.125f * 1.4426950408889634f;  // softmax scale * log2(e)
+  const float c = (SMALLHD || NH != 1) ? c_arg : 0.125f * 1.4426950408889634f;  // softmax scale * log2(e)
   const int nkw = (T + kKBlk - 1) / kKBlk;  // key-mask words per sequence
 
   ATTN_PROBE(0);
@@ -160,20 +163,18 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
 
   // iteration `it` computes from LDS buffer it&1, then stages tile it+1 (held in stage set
   // (it+1)&1 since two iterations ago) into the other buffer and refills that set with tile it+3
-  auto tile_step = [&](int it, ushort8_t(&st_next)[4]) __attribute__((always_inline)) {
+  auto tile_step = [&](int it, ushort8_t(&st_next)[2 * kCh]) __attribute__((always_inline)) {
     const int cur = it & 1;
     const bool more = it + 1 < ntiles;
     const int kbase = it * kKBlk;
     if (kbase <= q_hi) {
-      const bf16_raw* Kt = smem[cur][0];
-      const bf16_raw* Vt = smem[cur][1];
       f32x16 s[2];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         s[kt] = 0.f;
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const bf16x8 a = lds_row_read(Kt, kt * 32 + col, 2 * kk + half);
+        for (int kk = 0; kk < 4 * NH; ++kk) {
+          const bf16x8 a = lds_row_read(smem[cur][0][kk >> 2], kt * 32 + col, 2 * (kk & 3) + half);
           s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[kk], s[kt], 0, 0, 0);
         }
       }
@@ -216,8 +217,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
         // (KMASK: a lane still without any real key has m_new = -inf; -inf - -inf would be NaN)
         const float alpha = (KMASK && m_new == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f((m_run - m_new) * c);
         l_run *= alpha;
-        o[0] *= alpha;
-        o[1] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 2 * NH; ++dt) o[dt] *= alpha;
         m_run = m_new;
       }
       // an all-masked row so far (KMASK only) has m = -inf: offset 0 gives P = 0, not NaN
@@ -251,8 +252,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
         for (int st = 0; st < 2; ++st) {
           const bf16x8 pb = pack_acc8(s[kt], st);
 #pragma unroll
-          for (int dt = 0; dt < 2; ++dt) {
-            const bf16x8 va = lds_tr_read_operand(Vt, kt * 32 + 16 * st + 4 * half, dt * 32, lane);
+          for (int dt = 0; dt < 2 * NH; ++dt) {
+            const bf16x8 va = lds_tr_read_operand(smem[cur][1][dt >> 1], kt * 32 + 16 * st + 4 * half, (dt & 1) * 32, lane);
             o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o[dt], 0, 0, 0);
           }
         }
@@ -275,7 +276,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
     const float inv_l = dead ? 0.f : 1.f / l_run;
     bf16_raw* dst = out + ((long)b * T + q) * H * hd + (long)h * hd;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
+    for (int dt = 0; dt < 2 * NH; ++dt) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         ushort4_t v;
@@ -299,23 +300,33 @@ void attn_probe_set(unsigned long long* buf) {
 }
 #endif
 
-template <bool DROPOUT, bool KMASK, bool SMALLHD>
+template <bool DROPOUT, bool KMASK, bool SMALLHD, int NH = 1>
 static void launch_fwd_variant(dim3 grid, hipStream_t stream, const bf16_raw* qkv, bf16_raw* out, float* lse,
                                const AttnDims& d, int nqb, DropoutArgs dr) {
-  hipLaunchKernelGGL((attn::attn_fwd_kernel<DROPOUT, KMASK, SMALLHD>), grid, dim3(256), 0, stream, qkv, out, lse, d.T,
-                     d.H, nqb, dr, d.hd, d.scale * 1.4426950408889634f, d.key_bits);
+  hipLaunchKernelGGL((attn::attn_fwd_kernel<DROPOUT, KMASK, SMALLHD, NH>), grid, dim3(256), 0, stream, qkv, out, lse,
+                     d.T, d.H, nqb, dr, d.hd, d.scale * 1.4426950408889634f, d.key_bits);
 }
 
 hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, const AttnDims& d, DropoutArgs dropout,
                            hipStream_t stream) {
-  if (d.B <= 0 || d.T <= 0 || d.H <= 0 || d.T > 65535 || d.hd <= 0 || d.hd > attn::kHD || d.hd % 8 != 0)
+  const bool hd128 = d.hd == 2 * attn::kHD;
+  if (d.B <= 0 || d.T <= 0 || d.H <= 0 || d.T > 65535 || d.hd <= 0 || (d.hd > attn::kHD && !hd128) || d.hd % 8 != 0)
     return hipErrorInvalidValue;
   const int nqb = (d.T + attn::kQBlk - 1) / attn::kQBlk;
   dim3 grid(d.B * d.H, nqb);
-  const bool drop = dropout.thr != 0, km = d.key_bits != nullptr, small = d.hd != attn::kHD;
+  const bool drop = dropout.thr != 0, km = d.key_bits != nullptr, small = d.hd < attn::kHD;
   const int variant = (drop ? 4 : 0) | (km ? 2 : 0) | (small ? 1 : 0);
   auto q = (const bf16_raw*)qkv;
   auto o = (bf16_raw*)out;
+  if (hd128) {
+    switch (variant) {
+      case 0: launch_fwd_variant<false, false, false, 2>(grid, stream, q, o, lse, d, nqb, dropout); break;
+      case 2: launch_fwd_variant<false, true, false, 2>(grid, stream, q, o, lse, d, nqb, dropout); break;
+      case 4: launch_fwd_variant<true, false, false, 2>(grid, stream, q, o, lse, d, nqb, dropout); break;
+      default: launch_fwd_variant<true, true, false, 2>(grid, stream, q, o, lse, d, nqb, dropout); break;
+    }
+    return hipGetLastError();
+  }
   switch (variant) {
     case 0: launch_fwd_variant<false, false, false>(grid, stream, q, o, lse, d, nqb, dropout); break;
     case 1: launch_fwd_variant<false, false, true>(grid, stream, q, o, lse, d, nqb, dropout); break;

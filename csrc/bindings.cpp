@@ -308,14 +308,14 @@ void embedding_bwd(const Tensor& dx, const Tensor& ids, Tensor dwte, Tensor dwpe
 
 // ---- attention -------------------------------------------------------------------------------
 // head dim from the packed qkv [B*T, 3*H*hd]: a multiple of 8 up to 64 (the kernels' tiles are 64
-// wide; smaller heads are zero-filled in LDS/registers)
+// wide; smaller heads are zero-filled in LDS/registers) or exactly 128 (two 64-wide halves)
 int64_t attn_head_dim(const Tensor& qkv, int64_t B, int64_t T, int64_t H) {
   check_gpu(qkv, "qkv");
   check_dtype(qkv, at::kBFloat16, "qkv");
   TORCH_CHECK(B > 0 && T > 0 && H > 0 && qkv.numel() % (B * T * 3 * H) == 0, "qkv must be [B*T, 3*H*hd]");
   const int64_t hd = qkv.numel() / (B * T * 3 * H);
-  TORCH_CHECK(hd % 8 == 0 && hd >= 8 && hd <= 64, "attention kernels need head_dim % 8 == 0 and 8 <= head_dim <= 64, got ",
-              hd);
+  TORCH_CHECK((hd % 8 == 0 && hd >= 8 && hd <= 64) || hd == 128,
+              "attention kernels need head_dim % 8 == 0 and 8 <= head_dim <= 64, or head_dim == 128, got ", hd);
   return hd;
 }
 
@@ -380,7 +380,7 @@ Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const 
   } else {
     delta = at::empty({B, H, T}, lse.options());
   }
-  Tensor dq = at::empty({llmt::attn_bwd_workspace_floats((int)B, (int)T, (int)H)}, lse.options());
+  Tensor dq = at::empty({llmt::attn_bwd_workspace_floats((int)B, (int)T, (int)H, (int)hd)}, lse.options());
   Tensor bias_ws = workspace(lse, dbias.has_value() ? llmt::attn_bwd_bias_ws_floats((int)B, (int)T, (int)H, (int)hd) : 0);
   float* db = nullptr;
   if (dbias.has_value()) {

@@ -190,7 +190,7 @@ hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, const AttnDim
 // dqkv [B, T, 3, H, hd] bf16; optional `dbias` [3*H*hd] f32 accumulates the column sums of dqkv
 // (the qkv projection's bias gradient); `delta` [B, H, T] f32 and `dq_part`
 // (attn_bwd_workspace_floats(B, T, H) floats) scratch
-long attn_bwd_workspace_floats(int B, int T, int H);
+long attn_bwd_workspace_floats(int B, int T, int H, int hd = 64);
 // delta_ready: `delta` already holds rowsum(dO * O) (the out-proj dX GEMM's epilogue 3, which
 // then also added the V part of `dbias`): the delta pass is skipped
 // `bias_ws` (attn_bwd_bias_ws_floats(B, T, H, hd) floats; required with `dbias`) holds the

@@ -169,7 +169,8 @@ class GPT(nn.Module):
         """Whether the fused engine covers this shape on ``device_type``.  On the GPU the
         flash-attention kernels take head dims that are multiples of 8 up to 64 (64 is the fast
         specialisation — GPT-2 124M and XL; the reference presets' 32 and 48 run zero-filled in
-        the same tiles) and key-padding masks; LayerNorm widths need d % 4 == 0,
+        the same tiles) or exactly 128 (two 64-wide halves; a 4-wave one-wave-per-
+        SIMD backward) and key-padding masks; LayerNorm widths need d % 4 == 0,
         d <= 2048.  Other shapes train on the module path.  On CPU the engine runs the reference
         ops, which take any shape.  Dropout is supported everywhere (counter-based masks fused into
         the embedding, add+LayerNorm and flash-attention kernels)."""
@@ -179,8 +180,7 @@ class GPT(nn.Module):
             return False
         hd = self.d_model // self.n_heads
         return (
-            hd % 8 == 0
-            and 8 <= hd <= 64
+            ((hd % 8 == 0 and 8 <= hd <= 64) or hd == 128)
             and self.d_model % 4 == 0
             and self.d_model <= 2048
             and self.d_ff % 8 == 0

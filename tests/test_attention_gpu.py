@@ -1,7 +1,7 @@
 """Flash-attention kernels (csrc/attention_{fwd,bwd}.hip) against an INDEPENDENT oracle: fp32
 autograd of eager attention (reference ``models/gpt.py:56-74``: scores / sqrt(hd), causal and
 key-padding masks, softmax, P V) on the same bf16 inputs — no kernel output (lse, O) is fed into
-the oracle.  Covers head dims 32 / 48 / 64 (the reference presets and GPT-2), GPT-2 XL's 25 heads,
+the oracle.  Covers head dims 32 / 48 / 64 (the reference presets and GPT-2) and 128, GPT-2 XL's 25 heads,
 a production-sized batch (B*T = 64K tokens), ragged T, and key-padding masks with left padding
 (query rows that see no valid key), right padding and holes."""
 
@@ -63,6 +63,9 @@ CASES = [
     (3, 256, 8, 48, "mixed"),
     (4, 128, 8, 32, "mixed"),  # the K8s ConfigMap model's attention with padding
     (2, 1024, 12, 64, "mixed"),
+    (2, 1024, 8, 128, None),  # head dim 128: two 64-wide halves, the 4-wave backward
+    (1, 70, 2, 128, None),
+    (3, 300, 4, 128, "mixed"),
 ]
 
 
@@ -137,3 +140,27 @@ def test_padding_does_not_change_valid_rows(gpu_device) -> None:
     prefix = qkv.view(B, T, -1)[:, :L].reshape(B * L, -1).contiguous()
     out_p, _ = hip().attn_fwd(prefix, B, L, H)
     torch.testing.assert_close(out.view(B, T, -1)[:, :L].float(), out_p.view(B, L, -1).float(), atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("hd", [64, 128])
+def test_attention_dropout_head_dims(gpu_device, hd: int) -> None:
+    """Probability dropout at head dims 64 and 128 against the counter-based torch reference
+    (``ops/reference.py``: the same keep mask, the undropped normaliser in lse)."""
+    from llmtrain.ops import reference as ref
+
+    g = torch.Generator(device="cpu").manual_seed(hd)
+    B, T, H = 2, 200, 3
+    qkv = torch.randn(B * T, 3 * hd * H, generator=g).to(torch.bfloat16)
+    dout = torch.randn(B * T, hd * H, generator=g).to(torch.bfloat16)
+    adrop = (0.25, ref.dropout_site_seed(11, 8))
+    out_g, lse_g = ops.attn_fwd(qkv.to(gpu_device), B, T, H, dropout=adrop)
+    out_r, lse_r = ref.attn_fwd(qkv, B, T, H, *adrop)
+    torch.testing.assert_close(lse_g.cpu(), lse_r, atol=2e-3, rtol=2e-3)
+    torch.testing.assert_close(out_g.cpu().float(), out_r.float(), atol=3e-2, rtol=3e-2)
+    dbias = torch.zeros(3 * hd * H, device=gpu_device)
+    dq_g = ops.attn_bwd(dout.to(gpu_device), qkv.to(gpu_device), out_g, lse_g, B, T, H, dropout=adrop,
+                        qkv_bias_grad=dbias).cpu().float()
+    dq_r = ref.attn_bwd(dout, qkv, out_g.cpu(), lse_g.cpu(), B, T, H, *adrop).float()
+    assert (dq_g - dq_r).abs().max().item() < 2e-2 * dq_r.abs().max().item()
+    want = dq_r.sum(dim=0)
+    assert (dbias.cpu() - want).abs().max().item() < 2e-2 * want.abs().max().item()

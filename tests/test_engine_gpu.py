@@ -55,6 +55,7 @@ PRESET_SHAPES = {
     "k8s_configmap": (50257, 128, 256, 6, 8, 1024),  # head dim 32
     "gpt_wikitext_ddp": (50257, 128, 256, 4, 4, 1024),  # head dim 64
     "gpt_wikitext_better": (50257, 256, 384, 12, 8, 1536),  # head dim 48
+    "head_dim_128": (50257, 256, 512, 4, 4, 2048),  # not a reference preset: the hd = 128 kernels
 }
 
 

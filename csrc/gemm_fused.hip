@@ -393,9 +393,23 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) bias_f[k] = bf2f(bv[k]);
     }
+    // EPI 2 / 3 read a bf16 operand (U = the GELU pre-activation / the attention output) per row
+    // segment: those loads run one m-fragment ahead, so a tile's epilogue pays one memory round
+    // trip instead of eight (each m-fragment used to load and wait on its own)
+    u32x4 uraw[2][2];
+    auto load_u = [&](int mf, u32x4(&dst)[2]) {
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int m = mw + 16 * mf + 8 * it + (lane >> 3);
+        const int uoff = (m < p.M && n < p.N) ? (m * p.ldu + n) * 2 : kOob;
+        dst[it] = __builtin_amdgcn_raw_buffer_load_b128(ru, uoff, 0, 0);
+      }
+    };
+    if (EPI >= 2) load_u(0, uraw[0]);
 #pragma unroll
     for (int mf = 0; mf < 8; ++mf) {
       __builtin_amdgcn_sched_barrier(0);
+      if (EPI >= 2 && mf + 1 < 8) load_u(mf + 1, uraw[(mf + 1) & 1]);
       {
         const int row = lane & 15;
 #pragma unroll
@@ -420,13 +434,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
       }
       asm volatile("" ::: "memory");
       if (EPI == 3) {
-        u32x4 oraw[2];
-#pragma unroll
-        for (int it = 0; it < 2; ++it) {
-          const int m = mw + 16 * mf + 8 * it + (lane >> 3);
-          const int uoff = (m < p.M && n < p.N) ? (m * p.ldu + n) * 2 : kOob;
-          oraw[it] = __builtin_amdgcn_raw_buffer_load_b128(ru, uoff, 0, 0);
-        }
+        const u32x4(&oraw)[2] = uraw[mf & 1];
 #pragma unroll
         for (int it = 0; it < 2; ++it) {
           __builtin_amdgcn_sched_barrier(0);
@@ -456,17 +464,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
                        "+v"(csum[5]), "+v"(csum[6]), "+v"(csum[7]));
         }
       } else if (EPI == 2) {
-        u32x4 uraw[2];
-#pragma unroll
-        for (int it = 0; it < 2; ++it) {
-          const int m = mw + 16 * mf + 8 * it + (lane >> 3);
-          const int uoff = (m < p.M && n < p.N) ? (m * p.ldu + n) * 2 : kOob;
-          uraw[it] = __builtin_amdgcn_raw_buffer_load_b128(ru, uoff, 0, 0);
-        }
 #pragma unroll
         for (int it = 0; it < 2; ++it) {
           __builtin_amdgcn_sched_barrier(0);  // one row segment at a time: bounded VGPR pressure
-          const ushort8_t uv = __builtin_bit_cast(ushort8_t, uraw[it]);
+          const ushort8_t uv = __builtin_bit_cast(ushort8_t, uraw[mf & 1][it]);
           float o[8];
 #pragma unroll
           for (int k = 0; k < 8; ++k) {

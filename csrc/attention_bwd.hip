@@ -213,6 +213,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
                                                           const bf16_raw* __restrict__ dout,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta,
+                                                          const bf16_raw* __restrict__ out_o,
                                                           bf16_raw* __restrict__ dqkv,
                                                           float* __restrict__ dq_part, float* __restrict__ vparts,
                                                           int T, int H, int nkb, DropoutArgs dr, int hd_arg,
@@ -250,6 +251,16 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
                                                                          (int)((T - 1) * out_stride + hd) * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t r_lse = __builtin_amdgcn_make_buffer_rsrc((void*)lse_bh, (short)0, T * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t r_del = __builtin_amdgcn_make_buffer_rsrc((void*)delta_bh, (short)0, T * 4, 0x00020000);
+  // fused delta (out_o != nullptr): each thread also stages the O chunk matching its dO chunk and
+  // the tile's delta[r] = sum_d dO O is formed at staging time — no separate delta pass over dO and
+  // O (the 2.5x re-read of O per query row across key blocks stays in L2: a pair's key blocks share
+  // an XCD); without dropout the key block 0 workgroup (it sees every query row) also forms the
+  // column sums of dO = the V part of the qkv-bias gradient, vparts[b][h * hd + d]
+  const bool fuse_delta = out_o != nullptr;  // kernel argument: uniform
+  const __amdgpu_buffer_rsrc_t r_o = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(fuse_delta ? out_o + (long)b * T * H * hd + (long)h * hd : dobase), (short)0,
+      fuse_delta ? (int)((T - 1) * out_stride + hd) * 2 : 0, 0x00020000);
+  const bool vsum = fuse_delta && !DROPOUT && vparts != nullptr && kb == 0;
 
   const uint32_t pseed = DROPOUT ? mix32(dr.seed + (uint32_t)bh * 0x9E3779B9u) : 0u;  // see attn fwd
   const int kblk0 = kb * kKvBlk;
@@ -280,32 +291,48 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
     for (int j = 0; j < 8; ++j) kt_lds[kt_off(16 * kk + 8 * half + j, 32 * wave + col)] = kv[j];
   }
 
-  // register staging of one 64-row Q/dO tile (+ its row constants): 2 chunks per thread
-  ushort8_t stg[2];
+  // register staging of one 64-row Q/dO tile (+ its row constants): thread t holds Q and dO (and,
+  // fusing delta, O) of row (t >> 3) & 63, chunk t & 7
+  ushort8_t stg[2], stg_o;
   float stc = 0.f;
+  float vcol[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // dO column sums (vsum)
   auto load_tile = [&](int q0) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int cidx = threadIdx.x + 512 * i;
-      const int r = (cidx >> 3) & 63, ch = cidx & 7;
-      const int qrow = q0 + r;
-      const bool live = !SMALLHD || ch * 8 < hd;
-      stg[i] = i == 0 ? buf_load16(r_q, live ? (int)(qrow * row_stride + ch * 8) * 2 : kOobOff)
-                      : buf_load16(r_do, live ? (int)(qrow * out_stride + ch * 8) * 2 : kOobOff);
-    }
-    if (threadIdx.x < 2 * kQTile) {
+    const int r = (threadIdx.x >> 3) & 63, ch = threadIdx.x & 7;
+    const int qrow = q0 + r;
+    const bool live = !SMALLHD || ch * 8 < hd;
+    stg[0] = buf_load16(r_q, live ? (int)(qrow * row_stride + ch * 8) * 2 : kOobOff);
+    stg[1] = buf_load16(r_do, live ? (int)(qrow * out_stride + ch * 8) * 2 : kOobOff);
+    if (fuse_delta) {
+      stg_o = buf_load16(r_o, live ? (int)(qrow * out_stride + ch * 8) * 2 : kOobOff);
+      if (threadIdx.x < kQTile) stc = buf_load_f32(r_lse, (q0 + threadIdx.x) * 4);
+    } else if (threadIdx.x < 2 * kQTile) {
       const int qq = q0 + (threadIdx.x & (kQTile - 1));
       stc = threadIdx.x < kQTile ? buf_load_f32(r_lse, qq * 4) : buf_load_f32(r_del, qq * 4);
     }
   };
   auto store_tile = [&](int buf) {
+    const int r = (threadIdx.x >> 3) & 63, ch = threadIdx.x & 7;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int cidx = threadIdx.x + 512 * i;
-      const int r = (cidx >> 3) & 63, ch = cidx & 7;
-      *reinterpret_cast<ushort8_t*>(&qd_lds[buf][i][tile_chunk_off(r, ch)]) = stg[i];
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<ushort8_t*>(&qd_lds[buf][i][tile_chunk_off(r, ch)]) = stg[i];
+    if (fuse_delta) {
+      // delta[r]: this thread's 8 products, then the row's 8 threads (consecutive lanes)
+      float a[8], o[8];
+      unpack8(stg[1], a);
+      unpack8(stg_o, o);
+      float dot = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        dot = fmaf(a[k], o[k], dot);
+        if (vsum) vcol[k] += a[k];  // rows past T load as zeros
+      }
+      dot += __shfl_xor(dot, 1, 64);
+      dot += __shfl_xor(dot, 2, 64);
+      dot += __shfl_xor(dot, 4, 64);
+      if (threadIdx.x < kQTile) rowc_lds[buf][threadIdx.x] = stc * 1.4426950408889634f;
+      if (ch == 0 && threadIdx.x < 8 * kQTile) rowc_lds[buf][kQTile + r] = dot;
+    } else if (threadIdx.x < 2 * kQTile) {
+      rowc_lds[buf][threadIdx.x] = threadIdx.x < kQTile ? stc * 1.4426950408889634f : stc;
     }
-    if (threadIdx.x < 2 * kQTile) rowc_lds[buf][threadIdx.x] = threadIdx.x < kQTile ? stc * 1.4426950408889634f : stc;
   };
 
   f32x16 dk[2], dv[2];
@@ -518,6 +545,24 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   // sum this block's 256 keys of dV^T — over the 32 lanes of each half, then over the 8 waves —
   // into this block's partial row vparts[b * nkb + kb][h * hd + d].
   BWD_PROBE(63);
+  if (vsum) {  // wave-uniform (kb, kernel arguments): column sums of dO over all rows of this (b, h)
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int off = 8; off < 64; off <<= 1) vcol[k] += __shfl_xor(vcol[k], off, 64);
+    if (lane < 8) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bias_red[wave][8 * lane + k] = vcol[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < hd) {
+      float acc = 0.f;
+#pragma unroll
+      for (int w = 0; w < kBwdWaves; ++w) acc += bias_red[w][threadIdx.x];
+      vparts[(long)b * (H * hd) + h * hd + threadIdx.x] = acc;
+    }
+    return;
+  }
   if (!DROPOUT || vparts == nullptr) return;
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt) {
@@ -1163,6 +1208,15 @@ __global__ __launch_bounds__(256, 1) void attn_bwd128_kernel(const bf16_raw* __r
 }  // namespace attn
 
 namespace {
+// LLMT_ATTN_BWD_WAVES=4 selects the 4-wave kernel for hd <= 64 (A/B; 18-22% slower, see
+// attn_bwd4_kernel); default the 8-wave kernel
+int bwd_waves() {
+  static const int waves = [] {
+    const char* e = std::getenv("LLMT_ATTN_BWD_WAVES");
+    return e && std::atoi(e) == 4 ? 4 : 8;
+  }();
+  return waves;
+}
 // key-block size of the backward: 256 (8-wave kernel) for hd <= 64, 128 for hd = 128
 int bwd_kvblk(int hd) { return hd == 2 * attn::kHD ? attn::kKv128 : attn::kKvBlk; }
 int bwd_plane_width(int hd) { return hd == 2 * attn::kHD ? 2 * attn::kHD : attn::kHD; }
@@ -1201,19 +1255,14 @@ void attn_bwd_probe_set(unsigned long long* buf) {
 
 template <bool DROPOUT, bool KMASK, bool SMALLHD>
 static void launch_bwd_variant(dim3 grid, hipStream_t stream, const bf16_raw* qkv, const bf16_raw* dout,
-                               const float* lse, const float* delta, bf16_raw* dqkv, float* dq_part, float* vparts,
-                               const AttnDims& d, int nkb, DropoutArgs dr) {
-  // LLMT_ATTN_BWD_WAVES=4 selects the 4-wave kernel (A/B; 18-22% slower, see attn_bwd4_kernel)
-  static const int waves = [] {
-    const char* e = std::getenv("LLMT_ATTN_BWD_WAVES");
-    return e && std::atoi(e) == 4 ? 4 : 8;
-  }();
-  if (waves == 4)
+                               const float* lse, const float* delta, const bf16_raw* out_o, bf16_raw* dqkv,
+                               float* dq_part, float* vparts, const AttnDims& d, int nkb, DropoutArgs dr) {
+  if (bwd_waves() == 4)
     hipLaunchKernelGGL((attn::attn_bwd4_kernel<DROPOUT, KMASK, SMALLHD>), grid, dim3(256), 0, stream, qkv, dout, lse,
                        delta, dqkv, dq_part, vparts, d.T, d.H, nkb, dr, d.hd, d.scale, d.key_valid);
   else
     hipLaunchKernelGGL((attn::attn_bwd_kernel<DROPOUT, KMASK, SMALLHD>), grid, dim3(512), 0, stream, qkv, dout, lse,
-                       delta, dqkv, dq_part, vparts, d.T, d.H, nkb, dr, d.hd, d.scale, d.key_valid);
+                       delta, out_o, dqkv, dq_part, vparts, d.T, d.H, nkb, dr, d.hd, d.scale, d.key_valid);
 }
 
 hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse, void* dqkv,
@@ -1229,10 +1278,20 @@ hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, c
   float* vparts = dbias != nullptr ? bias_ws : nullptr;
   float* qparts = dbias != nullptr ? bias_ws + (long)bp.nv * bp.cols : nullptr;
   float* scratch = dbias != nullptr ? bias_ws + (long)(bp.nv + bp.nq) * bp.cols : nullptr;
+  // LLMT_ATTN_FUSED_DELTA=1: the 8-wave kernel forms delta (and, without dropout, the V-bias
+  // column sums) itself while staging each query tile instead of a separate delta pass.  Alone it
+  // is 2% faster at B=128 (1.085 vs 1.110 ms), but in the 124M step -0.4% (1.0555M vs 1.0596M
+  // tok/s, profiles/r2/ab_fused_delta.txt): the longer main kernel overlaps the side stream worse
+  // than the short delta pass, so the default is the separate pass.
+  static const bool fused_delta_env = [] {
+    const char* e = std::getenv("LLMT_ATTN_FUSED_DELTA");
+    return e && std::atoi(e) == 1;
+  }();
+  const bool fuse_delta = !delta_ready && !hd128 && bwd_waves() == 8 && fused_delta_env;
   const bool v_from_delta = !delta_ready && dropout.thr == 0 && dbias != nullptr;
   const dim3 dgrid((T + attn::kDeltaRows - 1) / attn::kDeltaRows, B * H);
   const bool small = hd < attn::kHD;
-  if (!delta_ready) {
+  if (!delta_ready && !fuse_delta) {
     auto dk = hd128 ? attn::attn_delta_kernel<false, 2>
                     : (small ? attn::attn_delta_kernel<true> : attn::attn_delta_kernel<false>);
     hipLaunchKernelGGL(dk, dgrid, dim3(256), 0, stream, (const bf16_raw*)dout, (const bf16_raw*)out, delta,
@@ -1246,7 +1305,10 @@ hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, c
   auto q = (const bf16_raw*)qkv;
   auto g = (const bf16_raw*)dout;
   auto dq = (bf16_raw*)dqkv;
-  float* vp = drop ? vparts : nullptr;  // the main kernel forms the V-bias partials only with dropout
+  // the main kernel forms the V-bias partials with dropout (per key block) and with the fused delta
+  // (key block 0's column sums of dO, one row per batch)
+  float* vp = (drop || (fuse_delta && v_from_delta)) ? vparts : nullptr;
+  const bf16_raw* out_o = fuse_delta ? (const bf16_raw*)out : nullptr;
   if (hd128) {
     auto k = drop ? (km ? attn::attn_bwd128_kernel<true, true> : attn::attn_bwd128_kernel<true, false>)
                   : (km ? attn::attn_bwd128_kernel<false, true> : attn::attn_bwd128_kernel<false, false>);
@@ -1254,14 +1316,14 @@ hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, c
                        d.key_valid);
   } else {
   switch (variant) {
-    case 0: launch_bwd_variant<false, false, false>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
-    case 1: launch_bwd_variant<false, false, true>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
-    case 2: launch_bwd_variant<false, true, false>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
-    case 3: launch_bwd_variant<false, true, true>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
-    case 4: launch_bwd_variant<true, false, false>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
-    case 5: launch_bwd_variant<true, false, true>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
-    case 6: launch_bwd_variant<true, true, false>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
-    default: launch_bwd_variant<true, true, true>(grid, stream, q, g, lse, delta, dq, dq_part, vp, d, nkb, dropout); break;
+    case 0: launch_bwd_variant<false, false, false>(grid, stream, q, g, lse, delta, out_o, dq, dq_part, vp, d, nkb, dropout); break;
+    case 1: launch_bwd_variant<false, false, true>(grid, stream, q, g, lse, delta, out_o, dq, dq_part, vp, d, nkb, dropout); break;
+    case 2: launch_bwd_variant<false, true, false>(grid, stream, q, g, lse, delta, out_o, dq, dq_part, vp, d, nkb, dropout); break;
+    case 3: launch_bwd_variant<false, true, true>(grid, stream, q, g, lse, delta, out_o, dq, dq_part, vp, d, nkb, dropout); break;
+    case 4: launch_bwd_variant<true, false, false>(grid, stream, q, g, lse, delta, out_o, dq, dq_part, vp, d, nkb, dropout); break;
+    case 5: launch_bwd_variant<true, false, true>(grid, stream, q, g, lse, delta, out_o, dq, dq_part, vp, d, nkb, dropout); break;
+    case 6: launch_bwd_variant<true, true, false>(grid, stream, q, g, lse, delta, out_o, dq, dq_part, vp, d, nkb, dropout); break;
+    default: launch_bwd_variant<true, true, true>(grid, stream, q, g, lse, delta, out_o, dq, dq_part, vp, d, nkb, dropout); break;
   }
   }
   const dim3 rgrid(B * H, (T + attn::kDqRows - 1) / attn::kDqRows);
@@ -1274,7 +1336,7 @@ hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, c
     // already added it) the V part; the K part of the qkv-bias gradient is exactly zero
     hipError_t e = launch_colsum_reduce(qparts, bp.nq, bp.cols, dbias, scratch, stream);
     if (e != hipSuccess) return e;
-    const int nv = drop ? B * nkb : (v_from_delta ? (int)dgrid.x * B : 0);
+    const int nv = drop ? B * nkb : (v_from_delta ? (fuse_delta ? B : (int)dgrid.x * B) : 0);
     if (nv > 0) {
       e = launch_colsum_reduce(vparts, nv, bp.cols, dbias + 2L * H * hd, scratch, stream);
       if (e != hipSuccess) return e;

@@ -584,337 +584,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
 }
 
 // ---------------------------------------------------------------------------------------------
-// 4-wave variant: one wave per SIMD, 64 keys per wave (two 32-key MFMA column blocks), the
-// playbook's attention-backward structure.  Per 64-row query tile the CU reads 256 KB from LDS
-// instead of the 8-wave kernel's 448 KB: the Q / dO A-operand reads of S and dP (row reads) and of
-// dV^T / dK^T (transposed reads) serve both key blocks of a wave, and the B operand of dQ = dS K
-// (this wave's 16 dQ columns over the block's 256 keys) stays in registers for the whole sweep,
-// read once from a K^T image; only dS^T crosses LDS.  512 registers per lane (arch VGPRs + AGPRs)
-// hold dK^T/dV^T of 64 keys (128), K/V fragments (64), the dQ B operand (32) and the S/dP tiles.
-// Same contract, masks, dropout and dQ partial planes as attn_bwd_kernel.
-constexpr int kB4Waves = 4;
-
-template <bool DROPOUT, bool KMASK, bool SMALLHD>
-__global__ __launch_bounds__(256, 1) void attn_bwd4_kernel(const bf16_raw* __restrict__ qkv,
-                                                           const bf16_raw* __restrict__ dout,
-                                                           const float* __restrict__ lse,
-                                                           const float* __restrict__ delta,
-                                                           bf16_raw* __restrict__ dqkv,
-                                                           float* __restrict__ dq_part, float* __restrict__ vparts,
-                                                           int T, int H, int nkb, DropoutArgs dr, int hd_arg,
-                                                           float scale_arg, const uint8_t* __restrict__ key_valid) {
-  __shared__ __attribute__((aligned(16))) bf16_raw qd_lds[2][2][kQTile * kHD];  // [buf][Q|dO] 32 KB
-  __shared__ __attribute__((aligned(16))) bf16_raw ds_lds[2][kKvBlk * kQTile];  // [buf][key][q] 64 KB
-  __shared__ __attribute__((aligned(16))) float rowc_lds[2][2 * kQTile];        // lse*log2e | delta
-  __shared__ float bias_red[kB4Waves][kHD];                                    // V bias (dropout)
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int half = lane >> 5, col = lane & 31;
-  int bh, kb;
-  chunked_dispatch(bh, kb);
-  const int b = bh / H, h = bh - b * H;
-  const int hd = SMALLHD ? hd_arg : kHD;
-  const long row_stride = 3L * H * hd;
-  const bf16_raw* base = qkv + (long)b * T * row_stride + (long)h * hd;
-  const bf16_raw* dobase = dout + (long)b * T * H * hd + (long)h * hd;
-  const long out_stride = (long)H * hd;
-  const float* lse_bh = lse + ((long)b * H + h) * T;
-  const float* delta_bh = delta + ((long)b * H + h) * T;
-  const __amdgpu_buffer_rsrc_t r_q = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0,
-                                                                        (int)((T - 1) * row_stride + hd) * 2, 0x00020000);
-  const __amdgpu_buffer_rsrc_t r_kv = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0,
-                                                                         (int)((T - 1) * row_stride + 3 * hd * H) * 2,
-                                                                         0x00020000);
-  const __amdgpu_buffer_rsrc_t r_do = __builtin_amdgcn_make_buffer_rsrc((void*)dobase, (short)0,
-                                                                         (int)((T - 1) * out_stride + hd) * 2, 0x00020000);
-  const __amdgpu_buffer_rsrc_t r_lse = __builtin_amdgcn_make_buffer_rsrc((void*)lse_bh, (short)0, T * 4, 0x00020000);
-  const __amdgpu_buffer_rsrc_t r_del = __builtin_amdgcn_make_buffer_rsrc((void*)delta_bh, (short)0, T * 4, 0x00020000);
-
-  const uint32_t pseed = DROPOUT ? mix32(dr.seed + (uint32_t)bh * 0x9E3779B9u) : 0u;
-  const int kblk0 = kb * kKvBlk;
-  const int kw0 = kblk0 + 64 * wave;  // first key of this wave; key block j = keys kw0 + 32 j ..
-  const float scale = SMALLHD ? scale_arg : 0.125f;
-  const float c = scale * 1.4426950408889634f;
-
-  int key[2];
-  bool kvalid[2];
-  bf16x8 kf[2][4], vf[2][4];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    key[j] = kw0 + 32 * j + col;
-    kvalid[j] = !KMASK || (key[j] < T && key_valid[(long)b * T + key[j]] != 0);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const bool live = !SMALLHD || 16 * kk + 8 * half < hd;
-      const int off = (int)(key[j] * row_stride + 16 * kk + 8 * half) * 2;
-      kf[j][kk] = __builtin_bit_cast(bf16x8, buf_load16(r_kv, live ? off + hd * H * 2 : kOobOff));
-      vf[j][kk] = __builtin_bit_cast(bf16x8, buf_load16(r_kv, live ? off + 2 * hd * H * 2 : kOobOff));
-    }
-  }
-  // dQ B operand (16x16x32, k = key, n = d): lane l holds K[32 ks + 8 (l >> 4) + 0..7][16 w + (l & 15)],
-  // read once through a K^T image [64 d][256 keys] built in the second dS buffer (free until the
-  // second query tile, i.e. after the loop's first barrier)
-  bf16x8 kq[kKvBlk / 32];
-  {
-    bf16_raw* kt_img = ds_lds[1];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const ushort8_t kv = __builtin_bit_cast(ushort8_t, kf[j][kk]);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) kt_img[kt_off(16 * kk + 8 * half + e, 64 * wave + 32 * j + col)] = kv[e];
-      }
-    __syncthreads();
-#pragma unroll
-    for (int ks = 0; ks < kKvBlk / 32; ++ks)
-      kq[ks] = *reinterpret_cast<const bf16x8*>(&kt_img[kt_off(16 * wave + (lane & 15), 32 * ks + 8 * (lane >> 4))]);
-  }
-
-  // register staging of one 64-row Q/dO tile (+ row constants): 4 chunks per thread
-  ushort8_t stg[4];
-  float stc = 0.f;
-  auto load_tile = [&](int q0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int cidx = threadIdx.x + 256 * (i & 1);
-      const int r = cidx >> 3, ch = cidx & 7;
-      const int qrow = q0 + r;
-      const bool live = !SMALLHD || ch * 8 < hd;
-      stg[i] = i < 2 ? buf_load16(r_q, live ? (int)(qrow * row_stride + ch * 8) * 2 : kOobOff)
-                     : buf_load16(r_do, live ? (int)(qrow * out_stride + ch * 8) * 2 : kOobOff);
-    }
-    if (threadIdx.x < 2 * kQTile) {
-      const int qq = q0 + (threadIdx.x & (kQTile - 1));
-      stc = threadIdx.x < kQTile ? buf_load_f32(r_lse, qq * 4) : buf_load_f32(r_del, qq * 4);
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int cidx = threadIdx.x + 256 * (i & 1);
-      const int r = cidx >> 3, ch = cidx & 7;
-      *reinterpret_cast<ushort8_t*>(&qd_lds[buf][i >> 1][tile_chunk_off(r, ch)]) = stg[i];
-    }
-    if (threadIdx.x < 2 * kQTile) rowc_lds[buf][threadIdx.x] = threadIdx.x < kQTile ? stc * 1.4426950408889634f : stc;
-  };
-
-  f32x16 dk[2][2], dv[2][2];  // [key block][d tile]
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-      dk[j][dt] = 0.f;
-      dv[j][dt] = 0.f;
-    }
-
-  // phase A of one 32-row query sub-tile for both key blocks of the wave
-  auto phase_a = [&](bool full, int q0, const bf16_raw* q_lds, const bf16_raw* do_lds, const float* rowc,
-                     bf16_raw* dsimg) {
-#pragma unroll
-    for (int qs = 0; qs < 2; ++qs) {
-      const int qb0 = q0 + 32 * qs;
-      bool act[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) act[j] = full || (kw0 + 32 * j <= qb0 + 31 && kw0 + 32 * j < T && qb0 < T);
-      f32x16 p[2], dp[2], ds[2];
-      if (act[0] || act[1]) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          p[j] = 0.f;
-          dp[j] = 0.f;
-        }
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const bf16x8 qa = lds_row_read(q_lds, 32 * qs + col, 2 * kk + half);
-          const bf16x8 da = lds_row_read(do_lds, 32 * qs + col, 2 * kk + half);
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            p[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[j][kk], p[j], 0, 0, 0);
-            dp[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[j][kk], dp[j], 0, 0, 0);
-          }
-        }
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const f32x4 l2 = *reinterpret_cast<const f32x4*>(&rowc[32 * qs + 8 * rr + 4 * half]);
-          const f32x4 dd = *reinterpret_cast<const f32x4*>(&rowc[kQTile + 32 * qs + 8 * rr + 4 * half]);
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int r = 4 * rr + i;
-              p[j][r] = __builtin_amdgcn_exp2f(fmaf(p[j][r], c, -l2[i]));
-              if (DROPOUT) {
-                const uint32_t qq = (uint32_t)(qb0 + 4 * half + (r & 3) + 8 * (r >> 2));
-                const bool kp = drop_keep(pseed, dr.thr, qq * (uint32_t)T + (uint32_t)key[j]);
-                dp[j][r] = (kp ? dp[j][r] * dr.scale : 0.f) - dd[i];
-                // (p is masked below first; dV takes the dropped p, dS the undropped one)
-                ds[j][r] = kp ? dr.scale : 0.f;  // keep factor, applied to p after the masks
-              } else {
-                dp[j][r] -= dd[i];
-              }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          if (KMASK && !kvalid[j]) p[j] = 0.f;
-          if (!full && ((kw0 + 32 * j + 31 > qb0) || (kw0 + 32 * j + 32 > T) || (qb0 + 32 > T))) {
-            const int lo = key[j] - qb0 - 4 * half, hi = T - 1 - qb0 - 4 * half;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int roff = (r & 3) + 8 * (r >> 2);
-              p[j][r] = (roff < lo || roff > hi) ? 0.f : p[j][r];
-            }
-          }
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            if (DROPOUT) {
-              const float keep = ds[j][r];
-              ds[j][r] = p[j][r] * dp[j][r];
-              p[j][r] = p[j][r] * keep;
-            } else {
-              ds[j][r] = p[j][r] * dp[j][r];
-            }
-          }
-        }
-        // dV^T += dO^T P ; dK^T += Q^T dS — the transposed A operands serve both key blocks
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-#pragma unroll
-          for (int dt = 0; dt < 2; ++dt) {
-            const bf16x8 doa = lds_tr_read_operand(do_lds, 32 * qs + 16 * st + 4 * half, dt * 32, lane);
-            const bf16x8 qa = lds_tr_read_operand(q_lds, 32 * qs + 16 * st + 4 * half, dt * 32, lane);
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              dv[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(doa, pack_acc8(p[j], st), dv[j][dt], 0, 0, 0);
-              dk[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, pack_acc8(ds[j], st), dk[j][dt], 0, 0, 0);
-            }
-          }
-        }
-      } else {
-        ds[0] = 0.f;
-        ds[1] = 0.f;
-      }
-      // dS^T image [key][q]
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int kl = 64 * wave + 32 * j + col;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          ushort4_t v;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = f2bf(ds[j][4 * g + i]);
-          *reinterpret_cast<ushort4_t*>(&dsimg[tile_elem_off(kl, 32 * qs + 8 * g + 4 * half)]) = v;
-        }
-      }
-    }
-  };
-
-  BWD_PROBE(0);
-  load_tile(kblk0);
-  store_tile(0);
-  __syncthreads();
-  BWD_PROBE(1);
-
-  int it = 0;
-  for (int q0 = kblk0; q0 < T; q0 += kQTile, ++it) {
-    const int cur = it & 1;
-    const bool more = q0 + kQTile < T;
-    if (more) load_tile(q0 + kQTile);
-    phase_a(q0 >= kblk0 + kKvBlk && q0 + kQTile <= T, q0, qd_lds[cur][0], qd_lds[cur][1], rowc_lds[cur], ds_lds[cur]);
-    BWD_PROBE(2 + 3 * it);
-    if (more) store_tile(cur ^ 1);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    BWD_PROBE(3 + 3 * it);
-
-    // ---- dQ[q0 + 16 qt + .., 16 w + (0..15)] = dS K over the block's 256 keys (16x16x32) ----
-    {
-      const int i = lane & 15, g = lane >> 4;
-      const bf16_raw* dsimg = ds_lds[cur];
-      f32x4 acc[4];
-#pragma unroll
-      for (int qt = 0; qt < 4; ++qt) acc[qt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      typedef short short8v __attribute__((ext_vector_type(8)));
-#pragma unroll
-      for (int ks = 0; ks < kKvBlk / 32; ++ks) {
-        const int krow = 32 * ks + 8 * g + (i >> 2);
-#pragma unroll
-        for (int qt = 0; qt < 4; ++qt) {
-          const int qcol = 16 * qt + 4 * (i & 3);
-          const short4v a_lo = tr_read(dsimg, krow, qcol);
-          const short4v a_hi = tr_read(dsimg, krow + 4, qcol);
-          const short8v a8 = {a_lo[0], a_lo[1], a_lo[2], a_lo[3], a_hi[0], a_hi[1], a_hi[2], a_hi[3]};
-          acc[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a8), kq[ks], acc[qt], 0, 0, 0);
-        }
-      }
-      // bf16 partial plane: lanes i, i^1 swap rows so each stores dwords (two adjacent columns)
-      const int p = i & 1;
-      const int dcol = 16 * wave + (i & ~1);
-      bf16_raw* plane = reinterpret_cast<bf16_raw*>(dq_part) + ((long)kb * gridDim.x + bh) * T * kHD;
-#pragma unroll
-      for (int qt = 0; qt < 4; ++qt) {
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          const int r = p ? 2 + jj : jj;
-          const int qq = q0 + 16 * qt + 4 * g + r;
-          const float sw = swap_pair(p ? acc[qt][jj] : acc[qt][2 + jj]);
-          const float own = p ? acc[qt][2 + jj] : acc[qt][jj];
-          const uint32_t w = (uint32_t)f2bf((p ? sw : own) * scale) | ((uint32_t)f2bf((p ? own : sw) * scale) << 16);
-          if (qq < T) *reinterpret_cast<uint32_t*>(plane + (long)qq * kHD + dcol) = w;
-        }
-      }
-    }
-    BWD_PROBE(4 + 3 * it);
-  }
-
-  // ---- dK = scale * dK^T, dV = dV^T -> dqkv[b, key, 1|2, h, :] ----
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    if (key[j] < T) {
-      bf16_raw* dst = dqkv + ((long)b * T + key[j]) * row_stride + (long)h * hd;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          ushort4_t kv, vv;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            kv[i] = f2bf(dk[j][dt][4 * g + i] * scale);
-            vv[i] = f2bf(dv[j][dt][4 * g + i]);
-          }
-          const int d = dt * 32 + 8 * g + 4 * half;
-          if (!SMALLHD || d < hd) {
-            *reinterpret_cast<ushort4_t*>(dst + hd * H + d) = kv;
-            *reinterpret_cast<ushort4_t*>(dst + 2 * hd * H + d) = vv;
-          }
-        }
-      }
-    }
-  }
-  BWD_PROBE(63);
-  // V part of the qkv-bias gradient with dropout: this block's 256 keys of dV^T (see attn_bwd_kernel)
-  if (!DROPOUT || vparts == nullptr) return;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float vv = dv[0][dt][r] + dv[1][dt][r];
-#pragma unroll
-      for (int off = 1; off < 32; off <<= 1) vv += __shfl_xor(vv, off, 64);
-      if (col == 0) bias_red[wave][dt * 32 + 8 * (r >> 2) + 4 * half + (r & 3)] = vv;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < hd) {
-    float acc = 0.f;
-#pragma unroll
-    for (int w = 0; w < kB4Waves; ++w) acc += bias_red[w][threadIdx.x];
-    vparts[((long)b * nkb + kb) * (H * hd) + h * hd + threadIdx.x] = acc;
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // Head dim 128: 4 waves (one per SIMD, 512 registers per lane) x 32 keys = a 128-key block.  The
 // 8-wave kernel's per-wave state doubles at hd = 128 (dK^T / dV^T 128 registers, K/V fragments 64)
 // and no longer fits two waves per SIMD; here each wave keeps dK^T / dV^T of its 32 keys over the
@@ -1208,15 +877,6 @@ __global__ __launch_bounds__(256, 1) void attn_bwd128_kernel(const bf16_raw* __r
 }  // namespace attn
 
 namespace {
-// LLMT_ATTN_BWD_WAVES=4 selects the 4-wave kernel for hd <= 64 (A/B; 18-22% slower, see
-// attn_bwd4_kernel); default the 8-wave kernel
-int bwd_waves() {
-  static const int waves = [] {
-    const char* e = std::getenv("LLMT_ATTN_BWD_WAVES");
-    return e && std::atoi(e) == 4 ? 4 : 8;
-  }();
-  return waves;
-}
 // key-block size of the backward: 256 (8-wave kernel) for hd <= 64, 128 for hd = 128
 int bwd_kvblk(int hd) { return hd == 2 * attn::kHD ? attn::kKv128 : attn::kKvBlk; }
 int bwd_plane_width(int hd) { return hd == 2 * attn::kHD ? 2 * attn::kHD : attn::kHD; }
@@ -1257,12 +917,8 @@ template <bool DROPOUT, bool KMASK, bool SMALLHD>
 static void launch_bwd_variant(dim3 grid, hipStream_t stream, const bf16_raw* qkv, const bf16_raw* dout,
                                const float* lse, const float* delta, const bf16_raw* out_o, bf16_raw* dqkv,
                                float* dq_part, float* vparts, const AttnDims& d, int nkb, DropoutArgs dr) {
-  if (bwd_waves() == 4)
-    hipLaunchKernelGGL((attn::attn_bwd4_kernel<DROPOUT, KMASK, SMALLHD>), grid, dim3(256), 0, stream, qkv, dout, lse,
-                       delta, dqkv, dq_part, vparts, d.T, d.H, nkb, dr, d.hd, d.scale, d.key_valid);
-  else
-    hipLaunchKernelGGL((attn::attn_bwd_kernel<DROPOUT, KMASK, SMALLHD>), grid, dim3(512), 0, stream, qkv, dout, lse,
-                       delta, out_o, dqkv, dq_part, vparts, d.T, d.H, nkb, dr, d.hd, d.scale, d.key_valid);
+  hipLaunchKernelGGL((attn::attn_bwd_kernel<DROPOUT, KMASK, SMALLHD>), grid, dim3(512), 0, stream, qkv, dout, lse,
+                     delta, out_o, dqkv, dq_part, vparts, d.T, d.H, nkb, dr, d.hd, d.scale, d.key_valid);
 }
 
 hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse, void* dqkv,
@@ -1287,7 +943,7 @@ hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, c
     const char* e = std::getenv("LLMT_ATTN_FUSED_DELTA");
     return e && std::atoi(e) == 1;
   }();
-  const bool fuse_delta = !delta_ready && !hd128 && bwd_waves() == 8 && fused_delta_env;
+  const bool fuse_delta = !delta_ready && !hd128 && fused_delta_env;
   const bool v_from_delta = !delta_ready && dropout.thr == 0 && dbias != nullptr;
   const dim3 dgrid((T + attn::kDeltaRows - 1) / attn::kDeltaRows, B * H);
   const bool small = hd < attn::kHD;

@@ -506,8 +506,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
         csum[k] = v;
       }
       // this wave's 128-row block owns partial row mw / 128 of the column sums (plain stores; the
-      // launcher's fixed-order reduce adds the rows to the bias gradient: no atomics)
-      if (lane < 8 && n < p.N) {
+      // launcher's fixed-order reduce adds the rows to the bias gradient: no atomics).  Only
+      // ceil(M / 128) rows exist: a wave whose block lies wholly past M (the lower half of the
+      // last 256-row tile when M % 256 <= 128) has nothing to store
+      if (lane < 8 && n < p.N && mw < p.M) {
         float* dst = p.dbias + (long)(mw / 128) * p.N + n;
         *reinterpret_cast<float4_t*>(dst) = float4_t{csum[0], csum[1], csum[2], csum[3]};
         *reinterpret_cast<float4_t*>(dst + 4) = float4_t{csum[4], csum[5], csum[6], csum[7]};

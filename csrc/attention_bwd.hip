@@ -305,9 +305,11 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
     if (fuse_delta) {
       stg_o = buf_load16(r_o, live ? (int)(qrow * out_stride + ch * 8) * 2 : kOobOff);
       if (threadIdx.x < kQTile) stc = buf_load_f32(r_lse, (q0 + threadIdx.x) * 4);
-    } else if (threadIdx.x < 2 * kQTile) {
+    } else if (wave < 2) {
+      // wave 0: lse, wave 1: delta — a wave-uniform choice of descriptor (a per-lane select of the
+      // descriptor made hipcc emit a readfirstlane waterfall loop around the load, every tile)
       const int qq = q0 + (threadIdx.x & (kQTile - 1));
-      stc = threadIdx.x < kQTile ? buf_load_f32(r_lse, qq * 4) : buf_load_f32(r_del, qq * 4);
+      stc = wave == 0 ? buf_load_f32(r_lse, qq * 4) : buf_load_f32(r_del, qq * 4);
     }
   };
   auto store_tile = [&](int buf) {
@@ -680,9 +682,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd128_kernel(const bf16_raw* __r
       stg[i] = i < 4 ? buf_load16(r_q, (int)(qrow * row_stride + ch * 8) * 2)
                      : buf_load16(r_do, (int)(qrow * out_stride + ch * 8) * 2);
     }
-    if (threadIdx.x < 2 * kQTile) {
+    if (wave < 2) {  // wave 0: lse, wave 1: delta (wave-uniform descriptor choice)
       const int qq = q0 + (threadIdx.x & (kQTile - 1));
-      stc = threadIdx.x < kQTile ? buf_load_f32(r_lse, qq * 4) : buf_load_f32(r_del, qq * 4);
+      stc = wave == 0 ? buf_load_f32(r_lse, qq * 4) : buf_load_f32(r_del, qq * 4);
     }
   };
   auto store_tile = [&](int buf) {

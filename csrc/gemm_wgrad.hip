@@ -168,6 +168,136 @@ __global__ __launch_bounds__(kThreads, (Cfg<TN, TK>::kMinBlocks)) void wgrad_ker
   }
 }
 
+// The 256x256 tile as a software pipeline (default for tile 256; LLMT_WGRAD_PIPE=0 restores the
+// kernel above).  Counter passes on the kernel above (qkv at M = 131072, profiles/r2/) put the
+// MFMA pipe at 45 % busy: per 32-row stage a wave first issued its 8 LDS-DMA ops (each an asm
+// statement with a memory clobber, so no LDS read could move above them), then 20 fragment reads,
+// then waited lgkmcnt(0) before its first MFMA — ~1960 cycles per stage for 1024 of MFMA.
+// Here, per stage s:
+//   top:   s_waitcnt vmcnt(P) lgkmcnt(0) + barrier   (stage s+1 landed everywhere; this wave's
+//          reads of stage s, issued one stage earlier, are in registers)
+//   body:  8 groups of { 4 fragment reads of stage s+1 ; 4 MFMAs on stage s's registers ;
+//          1 LDS-DMA op of stage s+3 }, each group pinned in place by a sched_barrier
+// so the DMA issue and the next stage's LDS reads hide under the MFMAs and no read latency is
+// exposed.  Fragments are double-buffered in registers (64 + 64 VGPRs beside the 256 AGPR
+// accumulators); the stage loop is unrolled by two so the buffers swap by renaming.  DMAs past the
+// last stage re-read the last stage into a slot nobody reads again, keeping every wait uniform.
+namespace {
+constexpr int PT = 4;  // 32x32 tiles per wave edge (4 waves of 128x128 = a 256x256 tile)
+constexpr int PW = 64 * PT;
+constexpr int PA = BM * PW;               // elements per operand image per stage
+constexpr int PSLOT = 2 * PA;
+constexpr int PDMA = PA * 2 / 1024 / 4;   // 1-KiB DMA ops per wave per operand per stage (4)
+}  // namespace
+
+// PNS ring slots of 32 KiB: 4 (128 KiB, two stages in flight behind the one being read) or 5 (all
+// 160 KiB of LDS, three in flight)
+template <int PNS>
+__global__ __launch_bounds__(kThreads, 1) void wgrad_pipe_kernel(
+    const bf16_raw* __restrict__ A, int lda, const bf16_raw* __restrict__ B, int ldb, float* __restrict__ C,
+    int ldc, int M, int N, int K, int tiles, int tiles_k, int m_chunk, int nwg, float* __restrict__ slabs,
+    int stage_mask) {
+  __shared__ __attribute__((aligned(16))) bf16_raw smem[PNS * PSLOT];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int w = xcd_remap(blockIdx.x, nwg);
+  const int chunk = w / tiles, tile = w - chunk * tiles;
+  const int tile_n = tile / tiles_k, tile_k = tile - tile_n * tiles_k;
+  const int n0 = tile_n * PW, k0 = tile_k * PW;
+  LLMT_DASSERT(n0 < N && k0 < K);
+  const int m_begin = chunk * m_chunk;
+  const int rows = min(M - m_begin, m_chunk);
+  if (rows <= 0) return;
+  const int nst = (rows + BM - 1) / BM;
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(A + (long)m_begin * lda), (short)0, rows * lda * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(B + (long)m_begin * ldb), (short)0, rows * ldb * 2, 0x00020000);
+  constexpr int cp = PW / 8;  // 16-byte chunks per LDS row
+  int va[PDMA], vb[PDMA];
+#pragma unroll
+  for (int j = 0; j < PDMA; ++j) {
+    const int row = (wave * PDMA + j) * (1024 / (2 * PW)) + lane / cp;
+    const int c = (lane % cp) ^ ((row & 3) << 2);
+    va[j] = (row * lda + n0 + 8 * c) * 2;
+    vb[j] = (row * ldb + k0 + 8 * c) * 2;
+  }
+  const unsigned lds_base = (unsigned)(unsigned long)(lds_void*)smem;
+  // DMA op j (0..7: A ops then B ops) of stage `st` into ring slot `slot`
+  auto dma = [&](int j, int st, int slot) {
+    const unsigned dst = lds_base + (unsigned)(slot * PSLOT * 2);
+    if (j < PDMA) dma16(dst + (wave * PDMA + j) * 1024, va[j], ra, st * BM * lda * 2);
+    else dma16(dst + PA * 2 + (wave * PDMA + j - PDMA) * 1024, vb[j - PDMA], rb, st * BM * ldb * 2);
+  };
+
+  const int wn = wave >> 1, wk = wave & 1;
+  f32x16 acc[PT][PT];
+#pragma unroll
+  for (int i = 0; i < PT; ++i)
+#pragma unroll
+    for (int j = 0; j < PT; ++j) acc[i][j] = 0.f;
+
+  // fragment f of a stage (0..15): k-step f / 8, operand (f % 8) / 4 (A, B), tile f % 4
+  auto read = [&](bf16x8 (&fr)[16], int slot, int f) {
+    const bf16_raw* img = smem + slot * PSLOT + ((f & 4) ? PA : 0);
+    const int col0 = ((f & 4) ? wk : wn) * 32 * PT + 32 * (f & 3);
+    fr[f] = tr_frag<PW>(img, 16 * (f >> 3), col0, lane);
+  };
+
+  // prologue: stages 0..PNS-2 in flight, stage 0 landed, its fragments read
+#pragma unroll
+  for (int s = 0; s < PNS - 1; ++s)
+#pragma unroll
+    for (int j = 0; j < 2 * PDMA; ++j) dma(j, min(s, nst - 1), s);
+  bf16x8 f0[16], f1[16];
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * PDMA * (PNS - 2)) : "memory");
+#pragma unroll
+  for (int f = 0; f < 16; ++f) read(f0, 0, f);
+
+  // one stage: MFMAs on `cur` (stage s), reads of stage s+1 into `nxt`, DMAs of stage s+PNS-1
+  auto stage = [&](int s, bf16x8 (&cur)[16], bf16x8 (&nxt)[16]) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): cur is in registers
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * PDMA * (PNS - 3)) : "memory");
+    const int rs = (s + 1) % PNS, ds = (s + PNS - 1) % PNS, dst_stage = min(s + PNS - 1, nst - 1) & stage_mask;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {  // g = k-step * 4 + A tile i
+      read(nxt, rs, 2 * g);
+      read(nxt, rs, 2 * g + 1);
+      const int ks = g >> 2, i = g & 3;
+#pragma unroll
+      for (int j = 0; j < PT; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[8 * ks + i], cur[8 * ks + 4 + j], acc[i][j], 0, 0, 0);
+      dma(g, dst_stage, ds);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  int s = 0;
+  for (; s + 1 < nst; s += 2) {
+    stage(s, f0, f1);
+    stage(s + 1, f1, f0);
+  }
+  if (s < nst) stage(s, f0, f1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup ends
+
+  const int half = lane >> 5, col = lane & 31;
+#pragma unroll
+  for (int i = 0; i < PT; ++i) {
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int k = k0 + wk * 32 * PT + 32 * j + col;
+      if (k >= K) continue;
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int n = n0 + wn * 32 * PT + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * half;
+        if (n >= N) continue;
+        if (slabs != nullptr) slabs[((long)chunk * N + n) * K + k] = acc[i][j][rr];
+        else atomicAdd(C + (long)n * ldc + k, acc[i][j][rr]);
+      }
+    }
+  }
+}
+
 struct Plan {
   int tile = 0, split = 1, m_chunk = 0, tiles = 0, tiles_k = 0;
   double cost = 1e30;
@@ -272,7 +402,24 @@ hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, fl
   if (det && det_ws == nullptr) return hipErrorInvalidValue;
   float* slabs = det ? det_ws : nullptr;
   const int nwg = p.tiles * p.split;
-  if (p.tile == 256) {
+  // LLMT_WGRAD_PIPE: ring slots of the pipelined 256-tile kernel (4 or 5), 0 = the plain kernel
+  static const int pipe = [] {
+    const char* e = std::getenv("LLMT_WGRAD_PIPE");
+    return e ? std::atoi(e) : 4;
+  }();
+  // LLMT_WGRAD_DEBUG=1 (timing experiments only, wrong results): every stage re-reads stage 0,
+  // so the operand stream is L2-resident and the kernel shows its compute + LDS + issue floor
+  static const int stage_mask = [] {
+    const char* e = std::getenv("LLMT_WGRAD_DEBUG");
+    return (e && e[0] == '1') ? 0 : -1;
+  }();
+  if (p.tile == 256 && pipe == 5) {
+    hipLaunchKernelGGL(wgrad::wgrad_pipe_kernel<5>, dim3(nwg), dim3(wgrad::kThreads), 0, stream, (const bf16_raw*)dy,
+                       lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k, p.m_chunk, nwg, slabs, stage_mask);
+  } else if (p.tile == 256 && pipe != 0) {
+    hipLaunchKernelGGL(wgrad::wgrad_pipe_kernel<4>, dim3(nwg), dim3(wgrad::kThreads), 0, stream, (const bf16_raw*)dy,
+                       lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k, p.m_chunk, nwg, slabs, stage_mask);
+  } else if (p.tile == 256) {
     hipLaunchKernelGGL((wgrad::wgrad_kernel<4, 4>), dim3(nwg), dim3(wgrad::kThreads), 0, stream,
                        (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k,
                        p.m_chunk, nwg, slabs);

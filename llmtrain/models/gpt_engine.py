@@ -115,6 +115,11 @@ class _StepState:
     muf: torch.Tensor | None = None
     rsf: torch.Tensor | None = None
     dlogits: torch.Tensor | None = None
+    # row-chunked LM head (FusedGPTEngine._head_chunked): dhf = dlogits @ W formed in the forward,
+    # the unscaled head weight gradient (side stream) and the chunk buffers / events it reads
+    dhf: torch.Tensor | None = None
+    head_dw: torch.Tensor | None = None
+    head_hold: Any = None
     drop_p: float = 0.0
     drop_seed: int = 0
     # key-padding mask (reference gpt.py:60-64, 73-74): the attention kernels' key masks and the
@@ -206,6 +211,12 @@ class FusedGPTEngine:
         self.head_wgrad_side = os.environ.get("LLMTRAIN_HEAD_WGRAD_SIDE", "0") == "1"
         # A/B knob: LLMTRAIN_HEAD_SCALE_FUSED=0 restores the three-pass torch rescale of hf
         self.fused_head_scale = os.environ.get("LLMTRAIN_HEAD_SCALE_FUSED", "1") != "0"
+        # rows per LM-head chunk (0 = whole micro-batch, the default; -1 = automatic): the memory mode
+        # of _head_chunked.  Same-box at micro-batch 128 it costs 3 % (1.021M vs 1.053M tok/s,
+        # profiles/r2/head_chunk_ab.txt): the per-chunk dX GEMM (M = 16K, N = 768, K = 50304) runs
+        # 3x slower than its share of the whole one while the side stream's chunk weight gradient
+        # holds the CUs — both are compute-bound, so the overlap buys nothing
+        self.head_chunk_rows = int(os.environ.get("LLMTRAIN_HEAD_CHUNK_ROWS", "0"))
 
     # ------------------------------------------------------------------------------------
 
@@ -361,14 +372,74 @@ class FusedGPTEngine:
             x, delta, m.ln_f.weight, m.ln_f.bias, self.eps, cdt, dropout=state.site(3 * n_layers)
         )
         head = self.store.shadow_of(self.head_weight, padded=True)
-        logits = torch.mm(hf, head.t())  # [M, Vp]
-        per_row = ops.cross_entropy_fwd_bwd(logits, labels.reshape(-1), self.vocab, row_w)
-        loss = torch.dot(per_row, row_w)
+        rows = self._head_chunk_rows(n_tok) if hf.is_cuda else 0
+        if rows:
+            loss = self._head_chunked(state, hf, head, labels.reshape(-1), row_w, rows, keep)
+        else:
+            logits = torch.mm(hf, head.t())  # [M, Vp]
+            per_row = ops.cross_entropy_fwd_bwd(logits, labels.reshape(-1), self.vocab, row_w)
+            loss = torch.dot(per_row, row_w)
+            if keep:
+                state.dlogits = logits
         self._pop()
         if keep:
             state.xf, state.hf, state.muf, state.rsf = xf, hf, muf, rsf
-            state.dlogits = logits
         return loss, state
+
+    def _head_chunk_rows(self, n_tok: int) -> int:
+        """Rows per LM-head chunk (0 = the whole micro-batch at once).  ``-1`` (automatic) cuts a
+        micro-batch of at least two 16K-row chunks into up to 8 (hipBLASLt's head GEMM loses ~3 %
+        at 16K rows and ~20 % at 4K, profiles/r2/head_chunk_ce.log)."""
+        if self.head_chunk_rows >= 0:
+            rows = self.head_chunk_rows
+        else:
+            rows = max(16384, -(-n_tok // 8))
+        return rows if 0 < rows < n_tok else 0
+
+    def _head_chunked(self, st, hf, head, labels, row_w, rows: int, keep: bool) -> torch.Tensor:
+        """LM head + fused cross-entropy over row chunks, the [M, Vp] logits never materialised.
+
+        Per chunk on the main stream: ``logits_c = hf_c W^T`` (hipBLASLt), the CE kernel (loss rows
+        + dlogits in place), ``dhf_c = dlogits_c W``; the weight gradient ``dW += dlogits_c^T hf_c``
+        goes to the side stream into an fp32 buffer, overlapping the next chunk's GEMM and CE, so
+        the head's backward no longer serialises ~10 ms of split-K GEMM on the main stream.  The
+        upstream gradient is unknown in the forward: LayerNorm backward applies it to ``dhf`` as
+        before, and the backward adds ``go * dW`` to the head gradient (side stream).  Two chunk
+        buffers ping-pong; the main stream waits for the side stream before reusing one.  Peak
+        memory: 2 chunks instead of the 13.2 GB logits at 128K tokens (reference gpt.py:181-184,
+        trainer cross-entropy :256-269)."""
+        n_tok, vp = hf.shape[0], head.shape[0]
+        per_row = torch.empty(n_tok, dtype=torch.float32, device=hf.device)
+        side = self._side_stream() if keep else None
+        if keep:
+            st.dhf = torch.empty_like(hf)
+            st.head_dw = torch.zeros(self.vocab, hf.shape[1], dtype=torch.float32, device=hf.device)
+        nbuf = 2 if side is not None else 1
+        bufs = [torch.empty(rows, vp, dtype=hf.dtype, device=hf.device) for _ in range(nbuf)]
+        events: list[Any] = [None] * nbuf
+        main = torch.cuda.current_stream()
+        for c, r0 in enumerate(range(0, n_tok, rows)):
+            r1 = min(n_tok, r0 + rows)
+            k = c % nbuf
+            if events[k] is not None:
+                main.wait_event(events[k])  # the side stream is done reading this buffer
+            lc = bufs[k][: r1 - r0]
+            torch.mm(hf[r0:r1], head.t(), out=lc)
+            per_row[r0:r1] = ops.cross_entropy_fwd_bwd(lc, labels[r0:r1], self.vocab, row_w[r0:r1])
+            if not keep:
+                continue
+            torch.mm(lc, head, out=st.dhf[r0:r1])
+            if side is not None:
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    self._wgrad_now(st.head_dw, lc[:, : self.vocab], hf[r0:r1])
+                events[k] = torch.cuda.Event()
+                events[k].record(side)
+            else:
+                self._wgrad_now(st.head_dw, lc[:, : self.vocab], hf[r0:r1])
+        if keep:
+            st.head_hold = bufs  # read by the side stream: released after the backward joins it
+        return torch.dot(per_row, row_w)
 
     # -- backward --------------------------------------------------------------------------
 
@@ -387,9 +458,11 @@ class FusedGPTEngine:
             self.grad_ready(segment)
 
     def _backward(self, st: _StepState, grad_out: torch.Tensor) -> None:
-        m = self.model
-        bsz, seqlen = st.bsz, st.seqlen
         go = grad_out.detach().reshape(()).float()
+        if st.head_dw is not None:
+            dhf, held = self._head_chunked_bwd(st, go)
+            self._backward_blocks(st, go, dhf, held)
+            return
         dlogits = st.dlogits
         assert dlogits is not None and st.hf is not None
         head = self.store.shadow_of(self.head_weight, padded=True)
@@ -422,7 +495,29 @@ class FusedGPTEngine:
         del hf_scaled
         st.dlogits = None
         del dlogits
+        self._pop()
+        self._backward_blocks(st, go, dhf, held)
 
+    def _head_chunked_bwd(self, st: _StepState, go: torch.Tensor) -> tuple[torch.Tensor, Any]:
+        """Backward of :meth:`_head_chunked`: ``grad(head) += go * dW`` on the side stream behind
+        the chunks' weight-gradient GEMMs (no main-stream wait); returns ``(dhf, held)``."""
+        g = self._g(self.head_weight)
+        if self._side is not None:
+            self._side.wait_stream(torch.cuda.current_stream())  # go
+            with torch.cuda.stream(self._side):
+                g.addcmul_(st.head_dw, go)
+        else:
+            g.addcmul_(st.head_dw, go)
+        dhf = st.dhf
+        held = (st.head_hold, st.head_dw, go)
+        st.dhf = st.head_dw = st.head_hold = None
+        return dhf, held
+
+    def _backward_blocks(self, st: _StepState, go: torch.Tensor, dhf: torch.Tensor, held: Any) -> None:
+        """Final LayerNorm and the transformer blocks, last to first, then the embeddings."""
+        m = self.model
+        bsz, seqlen = st.bsz, st.seqlen
+        self._push("bwd.ln_f")
         last = self.blocks[-1]
         n_layers = len(self.blocks)
         dx, dx_lp = ops.layernorm_bwd(

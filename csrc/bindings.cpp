@@ -412,7 +412,7 @@ Tensor dropout_mask(int64_t n, double p, int64_t seed, const Tensor& like) {
 }
 
 // ---- weight-gradient GEMM --------------------------------------------------------------------
-void wgrad_gemm(const Tensor& dy, const Tensor& x, Tensor c, int64_t split, int64_t tile) {
+void wgrad_gemm(const Tensor& dy, const Tensor& x, Tensor c, int64_t split, int64_t tile, int64_t pipe) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && c.is_cuda(), "wgrad_gemm: GPU tensors required");
   check_dtype(dy, at::kBFloat16, "dy");
   check_dtype(x, at::kBFloat16, "x");
@@ -428,7 +428,7 @@ void wgrad_gemm(const Tensor& dy, const Tensor& x, Tensor c, int64_t split, int6
   Tensor ws = workspace(c, det);
   check_hip(llmt::launch_wgrad_gemm(dy.data_ptr(), (int)dy.stride(0), x.data_ptr(), (int)x.stride(0),
                                     c.data_ptr<float>(), (int)c.stride(0), (int)M, (int)N, (int)K, (int)split,
-                                    (int)tile, cur_stream(), det > 0 ? ws.data_ptr<float>() : nullptr),
+                                    (int)tile, cur_stream(), det > 0 ? ws.data_ptr<float>() : nullptr, (int)pipe),
             "wgrad_gemm");
 }
 
@@ -578,7 +578,7 @@ TORCH_LIBRARY(llmtrain_hip, m) {
   m.def("dropout_mask(int n, float p, int seed, Tensor like) -> Tensor");
   m.def("set_deterministic(bool on) -> ()", &set_deterministic);  // catch-all: no tensor arguments
   m.def("get_deterministic() -> bool", &get_deterministic);
-  m.def("wgrad_gemm(Tensor dy, Tensor x, Tensor(a!) c, int split=0, int tile=0) -> ()");
+  m.def("wgrad_gemm(Tensor dy, Tensor x, Tensor(a!) c, int split=0, int tile=0, int pipe=-1) -> ()");
   m.def("gemm_fused(Tensor a, Tensor b, bool b_kn, int epilogue, Tensor? bias=None, Tensor? u=None,"
         " Tensor(a!)? dbias=None, int seq_len=0) -> (Tensor, Tensor?)");
   m.def("sumsq(Tensor x) -> Tensor");

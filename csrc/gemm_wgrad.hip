@@ -168,8 +168,11 @@ __global__ __launch_bounds__(kThreads, (Cfg<TN, TK>::kMinBlocks)) void wgrad_ker
   }
 }
 
-// The 256x256 tile as a software pipeline (default for tile 256; LLMT_WGRAD_PIPE=0 restores the
-// kernel above).  Counter passes on the kernel above (qkv at M = 131072, profiles/r2/) put the
+// The 256x256 tile as a software pipeline, for GEMMs that own the chip (launch_wgrad_gemm's
+// `pipe`; the LM head's weight gradient on the main stream).  It needs all 512 registers per lane,
+// so no other kernel's wave fits on its SIMDs — on the side stream that starved the main stream's
+// small kernels (a column sum queued ~490 us behind it) and cancelled the gain; the side stream
+// keeps the kernel above.  Counter passes on the kernel above (qkv at M = 131072, profiles/r2/) put the
 // MFMA pipe at 45 % busy: per 32-row stage a wave first issued its 8 LDS-DMA ops (each an asm
 // statement with a memory clobber, so no LDS read could move above them), then 20 fragment reads,
 // then waited lgkmcnt(0) before its first MFMA — ~1960 cycles per stage for 1024 of MFMA.
@@ -391,7 +394,7 @@ long wgrad_gemm_det_ws_floats(int lda, int ldb, int M, int N, int K, int split, 
 }
 
 hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N,
-                             int K, int split, int tile, hipStream_t stream, float* det_ws) {
+                             int K, int split, int tile, hipStream_t stream, float* det_ws, int pipe_req) {
   if (M <= 0 || N <= 0 || K <= 0) return hipSuccess;
   // N needs no alignment: tiles past N read the next rows' data (or zeros past the chunk) into
   // accumulators whose stores the epilogue masks with n < N (the LM head's N = 50257)
@@ -402,11 +405,12 @@ hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, fl
   if (det && det_ws == nullptr) return hipErrorInvalidValue;
   float* slabs = det ? det_ws : nullptr;
   const int nwg = p.tiles * p.split;
-  // LLMT_WGRAD_PIPE: ring slots of the pipelined 256-tile kernel (4 or 5), 0 = the plain kernel
-  static const int pipe = [] {
+  // LLMT_WGRAD_PIPE (A/B runs): forces the variant for every call, else the caller's choice
+  static const int pipe_env = [] {
     const char* e = std::getenv("LLMT_WGRAD_PIPE");
-    return e ? std::atoi(e) : 4;
+    return e ? std::atoi(e) : -1;
   }();
+  const int pipe = pipe_env >= 0 ? pipe_env : (pipe_req >= 0 ? pipe_req : 0);
   // LLMT_WGRAD_DEBUG=1 (timing experiments only, wrong results): every stage re-reads stage 0,
   // so the operand stream is L2-resident and the kernel shows its compute + LDS + issue floor
   static const int stage_mask = [] {

@@ -135,8 +135,12 @@ hipError_t launch_sumsq(const float* x, long long n, float* partials, float* out
 // Deterministic mode: `det_ws` (wgrad_gemm_det_ws_floats(...) floats) receives per-chunk partial
 // slabs that are reduced into C in a fixed order instead of the split-K atomics.
 long wgrad_gemm_det_ws_floats(int lda, int ldb, int M, int N, int K, int split, int tile);
+// `pipe`: 0 = the plain 256-tile kernel (332 registers per lane: other kernels' waves can share
+// its SIMDs — the side-stream default), 4 / 5 = the software-pipelined one with that many ring
+// slots (all 512 registers: nothing else runs beside it — for GEMMs that own the chip), -1 = the
+// LLMT_WGRAD_PIPE environment default (0).
 hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N,
-                             int K, int split, int tile, hipStream_t stream, float* det_ws = nullptr);
+                             int K, int split, int tile, hipStream_t stream, float* det_ws = nullptr, int pipe = -1);
 
 // ---- forward / data-gradient GEMM with fused epilogues (bf16 in, fp32 accumulate, bf16 out)
 // C[M, N] = epi(A[M, K] . op(B)); B is [N, ldb] (K contiguous, b_kn = false) or [K, ldb]

@@ -268,9 +268,9 @@ class FusedGPTEngine:
             old, _ = self._held.pop(0)
             torch.cuda.current_stream().wait_event(old)
 
-    def _wgrad_now(self, dst: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
+    def _wgrad_now(self, dst: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, exclusive: bool = False) -> None:
         if self.wgrad_impl == "hip":
-            ops.wgrad_accum(dst, dy, x)
+            ops.wgrad_accum(dst, dy, x, exclusive=exclusive)
         else:
             accumulate_wgrad(dst, dy, x)
 
@@ -487,7 +487,7 @@ class FusedGPTEngine:
         elif dlogits.is_cuda and dlogits.dtype == torch.bfloat16:
             # split-K MFMA kernel: 9.78 vs 10.34 ms for hipBLASLt's fp32-output GEMM at 128K tokens
             # (bench/head_wgrad.py; N = 50257 rows inside the 50304-wide padded logits)
-            self._wgrad_now(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled)
+            self._wgrad_now(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled, exclusive=True)
             held = None
         else:
             accumulate_wgrad(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled)

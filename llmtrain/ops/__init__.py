@@ -269,11 +269,15 @@ def linear_dx_attn(dy, w, att, seqlen: int, v_bias_grad=None, head_dim: int = 64
     return torch.mm(dy, w), None
 
 
-def wgrad_accum(dst, dy, x) -> None:
+def wgrad_accum(dst, dy, x, *, exclusive: bool = False) -> None:
     """``dst (fp32 [N, K]) += dy[M, N]^T @ x[M, K]`` — split-K MFMA GEMM with atomic fp32
-    accumulation on GPU (``dy`` may be a column slice with a larger row stride)."""
+    accumulation on GPU (``dy`` may be a column slice with a larger row stride).  ``exclusive``:
+    nothing runs beside this GEMM (the LM head's, on the main stream), so the software-pipelined
+    kernel that takes all 512 registers of every SIMD it lands on is used; side-stream weight
+    gradients keep the 332-register kernel so main-stream waves can share its CUs (with the
+    pipelined one the fc-bias column sum behind them waited ~490 us per layer)."""
     if _on_gpu(dst):
-        hip_ops().wgrad_gemm(dy, x, dst, 0, 0)
+        hip_ops().wgrad_gemm(dy, x, dst, 0, 0, 4 if exclusive else 0)
     else:
         dst.addmm_(dy.t().float(), x.float())
 

@@ -29,8 +29,8 @@
 //    while this tile's epilogue runs;
 //  * A image [256 m][64 k] and NT B image [256 n][64 k]: 128-byte rows (each 1-KiB LDS-DMA op
 //    moves 8 whole cache lines), 16-byte chunks XOR (row & 7) so every ds_read_b128 lane group of
-//    a 16x16x32 fragment read hits 16 distinct bank slots.  NN B image [64 k][256 n] with the
-//    wgrad swizzle, read transposed (ds_read_b64_tr_b16);
+//    a 16x16x32 fragment read hits 16 distinct bank slots.  NN B image [64 k][256 n] with
+//    the swz_nn swizzle, read transposed (ds_read_b64_tr_b16);
 //  * fragment reads are issued one MFMA sub-group (16 MFMAs) ahead; one wait + barrier per stage,
 //    placed before the last sub-group so the next stage's first fragments load under it;
 //  * MFMA srcA = B fragment, srcB = A fragment, so a lane's accumulator column is one output ROW
@@ -163,6 +163,18 @@ __device__ __forceinline__ void wait_ring(bool post) {
 
 __device__ __forceinline__ bf16x8 lds_b128(const bf16_raw* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
+// NN B image [64 k][256 n]: 16-byte chunk c of row r sits at chunk c ^ swz_nn(r).  The wgrad
+// swizzle 4 * (r & 3) alone leaves a 16x16x32 transposed fragment read 2-way conflicted: its lane
+// group {0-31} covers rows r0..r0+3 and r0+8..r0+11 (two chunks each) and rows 8 apart repeat the
+// same (r & 3) — 19 % of the kernel's LDS cycles were bank-conflict cycles at M = 131072
+// (profiles/r2/pmc_fgemm_dx_gelu_nn.txt).  Bit 3 of the row flips bit 1 of the chunk, so the 16
+// (row, chunk) pairs of every lane group land on 16 distinct 4-bank groups.
+__device__ __forceinline__ int swz_nn(int row) { return ((row & 3) << 2) ^ (((row >> 3) & 1) << 1); }
+template <int W>
+__device__ __forceinline__ int nn_off(int row, int col) {
+  return row * W + (((col >> 3) ^ swz_nn(row)) << 3) + (col & 7);
+}
+
 // 16x16x32 operand from a [k rows][W cols] image with k running down the rows: lane l -> column
 // col0 + (l & 15), elements j = 0..7 -> rows row0 + 8*(l >> 4) + j (two ds_read_b64_tr_b16: in
 // each 16-lane group lane 4q+p addresses row r+q, columns 4p..4p+3)
@@ -171,8 +183,8 @@ __device__ __forceinline__ bf16x8 tr_frag16(const bf16_raw* tile, int row0, int 
   const int i = lane & 15;
   const int row = row0 + 8 * (lane >> 4) + (i >> 2);
   const int col = col0 + 4 * (i & 3);
-  const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(tile + swz_off<W>(row, col)));
-  const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(tile + swz_off<W>(row + 4, col)));
+  const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(tile + nn_off<W>(row, col)));
+  const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(tile + nn_off<W>(row + 4, col)));
   const short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, v);
 }
@@ -235,9 +247,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
   }
 #pragma unroll
   for (int j = 0; j < kDmaB; ++j) {
-    if (NN) {  // [64 k][256 n]: 2 rows of 512 B per op, wgrad swizzle
+    if (NN) {  // [64 k][256 n]: 2 rows of 512 B per op, swz_nn swizzle
       const int row = (wave * kDmaB + j) * 2 + (lane >> 5);
-      const int c = (lane & 31) ^ ((row & 3) << 2);
+      const int c = (lane & 31) ^ swz_nn(row);
       vb[j] = (row * p.ldb + 8 * c) * 2;
     } else {
       const int row = (wave * kDmaB + j) * 8 + (lane >> 3);

@@ -205,6 +205,10 @@ class FusedGPTEngine:
         self.markers = os.environ.get("LLMTRAIN_ROCTX", "0") == "1" and self.store.device.type == "cuda"
         self._side: torch.cuda.Stream | None = None
         self._pending: list[torch.Tensor] = []  # operands of side-stream GEMMs of the current block
+        # A/B knob: block weight gradients (proj, fc, out, qkv) whose side-stream GEMM waits until
+        # the main stream has queued the next dX GEMM / LayerNorm backward (see _backward_blocks)
+        self.wgrad_defer = frozenset(filter(None, os.environ.get("LLMTRAIN_WGRAD_DEFER", "").split(",")))
+        self._deferred: list[tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = []
         self._held: list[tuple[Any, list[torch.Tensor]]] = []  # (side event, operands) per block
         # LM-head weight gradient on the side stream (LLMTRAIN_HEAD_WGRAD_SIDE=1; same-box A/B: no gain,
         # the 5 ms GEMM and the block kernels it would overlap both want the whole chip)
@@ -230,7 +234,7 @@ class FusedGPTEngine:
     def _g(self, p: torch.Tensor) -> torch.Tensor:
         return self.store.grad_of(p)
 
-    def _wgrad(self, dst: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
+    def _wgrad(self, dst: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, *, name: str = "") -> None:
         """Block weight gradients: the split-K MFMA kernel (``ops.wgrad_accum``) on GPU — it fills
         the chip on these M-deep reductions where hipBLASLt picks too few tiles — unless
         ``LLMTRAIN_WGRAD=hipblaslt`` selects the library GEMM for A/B runs.  On GPU it runs on the
@@ -241,13 +245,29 @@ class FusedGPTEngine:
             accumulate_wgrad(dst, dy, x)
             return
         side = self._side_stream()
-        if side is not None:
+        if side is not None and name in self.wgrad_defer:
+            self._deferred.append((dst, dy, x))  # released at the next _release_wgrads()
+            self._pending.extend((dy, x))
+        elif side is not None:
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
                 self._wgrad_now(dst, dy, x)
             self._pending.extend((dy, x))
         else:
             self._wgrad_now(dst, dy, x)
+
+    def _release_wgrads(self) -> None:
+        """Start the deferred weight gradients (LLMTRAIN_WGRAD_DEFER) on the side stream behind
+        everything the main stream has queued so far."""
+        if not self._deferred:
+            return
+        side = self._side_stream()
+        assert side is not None
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for dst, dy, x in self._deferred:
+                self._wgrad_now(dst, dy, x)
+        self._deferred = []
 
     def _retire_block(self) -> None:
         """End of one block's backward: fence its side-stream GEMMs with an event and release the
@@ -532,15 +552,16 @@ class FusedGPTEngine:
             self._push(f"bwd.block{i}")
             blk, a = self.blocks[i], st.blocks[i]
             # MLP: delta = g Wp^T + bp ; dx is d(delta) (bias grad already summed by the LN bwd)
-            self._wgrad(self._g(blk.mlp_proj.weight), dx_lp, a.g)
+            self._wgrad(self._g(blk.mlp_proj.weight), dx_lp, a.g, name="proj")
             if self.fused_gemm_bwd:  # GELU backward + fc bias grad in the dX GEMM's epilogue
                 du = ops.linear_dx_gelu_bwd(dx_lp, self._w(blk.mlp_proj.weight), a.u, self._g(blk.mlp_fc.bias))
             else:
                 dg = torch.mm(dx_lp, self._w(blk.mlp_proj.weight))
                 du = ops.gelu_bwd(dg, a.u, self._g(blk.mlp_fc.bias))
                 del dg
-            self._wgrad(self._g(blk.mlp_fc.weight), du, a.h2)
+            self._wgrad(self._g(blk.mlp_fc.weight), du, a.h2, name="fc")
             dh2 = torch.mm(du, self._w(blk.mlp_fc.weight))
+            self._release_wgrads()
             del du
             masked = st.keep_col is not None
             dxm, dy_lp = ops.layernorm_bwd(
@@ -553,7 +574,7 @@ class FusedGPTEngine:
                 dy_lp = dy_lp * st.keep_col
                 ops.colsum_accum(dy_lp, self._g(blk.attn.out_proj.bias))
             # attention output projection
-            self._wgrad(self._g(blk.attn.out_proj.weight), dy_lp, a.att)
+            self._wgrad(self._g(blk.attn.out_proj.weight), dy_lp, a.att, name="out")
             wo = self._w(blk.attn.out_proj.weight)
             attn_drop = st.site(2 + 3 * i)
             qkv_bg = self._g(blk.attn.qkv_proj.bias)
@@ -576,9 +597,10 @@ class FusedGPTEngine:
                 qkv_bias_grad=qkv_bg, delta=delta, key_masks=st.key_masks,
             )
             del datt
-            self._wgrad(self._g(blk.attn.qkv_proj.weight), dqkv, a.h1)
+            self._wgrad(self._g(blk.attn.qkv_proj.weight), dqkv, a.h1, name="qkv")
             wq = self._w(blk.attn.qkv_proj.weight)
             dh1 = ops.linear_dx(dqkv, wq) if self.fused_gemm_bwd else torch.mm(dqkv, wq)
+            self._release_wgrads()
             del dqkv
             prev_bias = self._g(self.blocks[i - 1].mlp_proj.bias) if i > 0 else None
             dx, dx_lp = ops.layernorm_bwd(

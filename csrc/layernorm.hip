@@ -105,6 +105,23 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
 
 constexpr int kBwdWaves = 4;
 
+// LLMT_LN_NT (A/B): non-temporal hints in the backward for the operands nothing else re-reads soon:
+// 1 = the saved residual-stream input xs and the incoming residual gradient (read once), 2 = also
+// the outgoing fp32 residual gradient.  The bf16 dy (just written by the dX GEMM) and dx_lp (read
+// next by the GEMMs) keep the default policy.  Same box at mb 128 (profiles/r2/ln_bwd_nt_ab.txt):
+// solo 0.320 / 0.321 / 0.298 ms, in the step 1.0626M / 1.0647M / 1.0628M tok/s — noise, so 0.
+#ifndef LLMT_LN_NT
+#define LLMT_LN_NT 0
+#endif
+__device__ __forceinline__ float4_t load4_nt(const float* p) {
+  if (LLMT_LN_NT >= 1) return __builtin_nontemporal_load(reinterpret_cast<const float4_t*>(p));
+  return *reinterpret_cast<const float4_t*>(p);
+}
+__device__ __forceinline__ void store4_nt(float* p, float4_t v) {
+  if (LLMT_LN_NT >= 2) __builtin_nontemporal_store(v, reinterpret_cast<float4_t*>(p));
+  else *reinterpret_cast<float4_t*>(p) = v;
+}
+
 // Raw (unconverted) row chunk: the next row's operands are prefetched into these registers while
 // the current row is reduced, so every wave keeps two rows of loads in flight (the reductions
 // and the dependent stores otherwise serialise one HBM round trip per row).
@@ -156,7 +173,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       const int c = lane + j * 64;
       if (c < nc) {
         ng[j] = load_raw4(dy + row * d + 4 * c);
-        nx[j] = load_raw4(xs + row * d + 4 * c);
+        nx[j] = load4_nt(xs + row * d + 4 * c);
       }
     }
   }
@@ -179,7 +196,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
         const int c = lane + j * 64;
         if (c < nc) {
           g[j] = load4(dy + row * d + 4 * c);
-          xh[j] = load4(xs + row * d + 4 * c);
+          xh[j] = load4_nt(xs + row * d + 4 * c);
         }
       }
     }
@@ -187,7 +204,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 #pragma unroll
       for (int j = 0; j < MAXC; ++j) {
         const int c = lane + j * 64;
-        if (c < nc) rr[j] = load4(dresid + row * d + 4 * c);
+        if (c < nc) rr[j] = load4_nt(dresid + row * d + 4 * c);
       }
     }
     if (kPrefetch) {
@@ -200,7 +217,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
           const int c = lane + j * 64;
           if (c < nc) {
             ng[j] = load_raw4(dy + nrow * d + 4 * c);
-            nx[j] = load_raw4(xs + nrow * d + 4 * c);
+            nx[j] = load4_nt(xs + nrow * d + 4 * c);
           }
         }
       }
@@ -225,7 +242,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       if (c < nc) {
         float4_t out = (g[j] * wv[j] - c1 - xh[j] * c2) * rs;
         if (dresid != nullptr) out += rr[j];
-        store4(dx + row * d + 4 * c, out);
+        store4_nt(dx + row * d + 4 * c, out);
         // the branch that fed this residual stream sees its dropout mask (forward: add_ln_fwd)
         float4_t br = out;
         if (dr.thr != 0) {

@@ -8,7 +8,11 @@ resume metadata (world size, data position); readers that do not know it ignore 
 
 Improvements over the reference: writes are atomic (``.tmp`` + ``os.replace``; a crash never
 leaves a truncated "latest" file) and loading always uses the safe ``weights_only=True``
-unpickler (never arbitrary code);
+unpickler (never arbitrary code); with ``async_write`` (the trainer's default on GPU) the step
+only pays a device-to-host snapshot into reused pinned buffers (GPT-2 XL: 18.7 GB at PCIe
+rates instead of a ~8 s synchronous ``torch.save``), and a background thread serialises and
+renames the file while training continues — one write in flight at a time, flushed by
+:meth:`CheckpointManager.wait` (the trainer calls it before returning or raising);
 the numpy types a reference checkpoint stores in ``rng_states["numpy"]`` are allow-listed
 explicitly so reference checkpoints still load.
 """
@@ -18,6 +22,7 @@ from __future__ import annotations
 import logging
 import os
 import random
+from concurrent.futures import Future, ThreadPoolExecutor
 from pathlib import Path
 from typing import Any, TypedDict
 
@@ -82,11 +87,57 @@ def capture_rng_states() -> dict[str, Any]:
     return states
 
 
+class _HostSnapshot:
+    """Copies every device tensor of a payload into pinned host buffers that are reused from one
+    save to the next (keyed by position in the payload), preserving storage aliasing (the tied
+    ``lm_head`` / ``token_embedding`` weights stay one tensor in the file)."""
+
+    def __init__(self) -> None:
+        self._buffers: dict[tuple[Any, ...], torch.Tensor] = {}
+        self._device_copies = False
+
+    def take(self, payload: Any) -> Any:
+        seen: dict[tuple[Any, ...], torch.Tensor] = {}
+        self._device_copies = False
+        out = self._walk(payload, (), seen)
+        if self._device_copies:
+            torch.cuda.current_stream().synchronize()  # the copies landed: the snapshot is consistent
+        return out
+
+    def _walk(self, obj: Any, key: tuple[Any, ...], seen: dict[tuple[Any, ...], torch.Tensor]) -> Any:
+        if isinstance(obj, torch.Tensor):
+            alias = (obj.untyped_storage().data_ptr(), obj.storage_offset(), tuple(obj.shape), tuple(obj.stride()),
+                     obj.dtype)
+            if alias in seen:
+                return seen[alias]
+            if not obj.is_cuda:  # a live host tensor (a CPU model's parameters): copy it too
+                seen[alias] = obj.detach().clone()
+                return seen[alias]
+            buf = self._buffers.get(key)
+            if buf is None or buf.shape != obj.shape or buf.dtype != obj.dtype:
+                buf = torch.empty(obj.shape, dtype=obj.dtype, pin_memory=True)
+                self._buffers[key] = buf
+            buf.copy_(obj, non_blocking=True)
+            seen[alias] = buf
+            self._device_copies = True
+            return buf
+        if isinstance(obj, dict):
+            return {k: self._walk(v, (*key, k), seen) for k, v in obj.items()}
+        if isinstance(obj, (list, tuple)):
+            items = [self._walk(v, (*key, i), seen) for i, v in enumerate(obj)]
+            return type(obj)(items) if isinstance(obj, list) else tuple(items)
+        return obj
+
+
 class CheckpointManager:
-    def __init__(self, checkpoint_dir: Path, keep_last_k: int = 3) -> None:
+    def __init__(self, checkpoint_dir: Path, keep_last_k: int = 3, *, async_write: bool = False) -> None:
         self._checkpoint_dir = Path(checkpoint_dir)
         self._keep_last_k = keep_last_k
         self._checkpoint_dir.mkdir(parents=True, exist_ok=True)
+        self._async = async_write
+        self._snapshot = _HostSnapshot() if async_write else None
+        self._pool: ThreadPoolExecutor | None = None
+        self._inflight: Future[Path] | None = None
 
     @property
     def directory(self) -> Path:
@@ -116,12 +167,29 @@ class CheckpointManager:
         if extra:
             payload["llmtrain_extra"] = extra
         path = self.path_for(step)
+        if not self._async:
+            return self._write(payload, path)
+        self.wait()  # one write in flight: its pinned buffers are about to be refilled
+        assert self._snapshot is not None
+        host = self._snapshot.take(payload)
+        if self._pool is None:
+            self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="llmtrain-ckpt")
+        self._inflight = self._pool.submit(self._write, host, path)
+        return path
+
+    def _write(self, payload: dict[str, Any], path: Path) -> Path:
         tmp = path.with_name(path.name + ".tmp")
         torch.save(payload, tmp)
         os.replace(tmp, path)
-        logger.info("checkpoint: saved step %d to %s", step, path)
+        logger.info("checkpoint: saved step %d to %s", payload["step"], path)
         self._prune_old()
         return path
+
+    def wait(self) -> None:
+        """Block until the asynchronous write in flight (if any) is on disk; re-raises its error."""
+        fut, self._inflight = self._inflight, None
+        if fut is not None:
+            fut.result()
 
     def load(self, path: Path, *, map_location: Any = "cpu") -> CheckpointPayload:
         logger.info("checkpoint: loading %s", path)

@@ -19,7 +19,8 @@ What changes on the MI355X path:
 * ``peak_memory`` reports ``torch.cuda.max_memory_allocated`` (GiB) on GPU;
 * optional ``trainer.extra``: ``keep_last_k``, ``fail_at_step`` / ``fail_rank`` (fault injection:
   that rank raises at that step of a run that did not resume — one simulated crash per job),
-  ``profile`` (torch.profiler window), ``bucket_cap_mb``, ``grad_reduce_dtype``;
+  ``profile`` (torch.profiler window), ``bucket_cap_mb``, ``grad_reduce_dtype``,
+  ``async_checkpoint`` (GPU default true: pinned snapshot + background write);
 * ``train/allreduce_ms`` (max over ranks) logs the exposed gradient all-reduce time of the flat
   reducer — the part of the communication NOT hidden behind the backward.
 """
@@ -196,7 +197,10 @@ class Trainer:
         self._ckpt_mgr: CheckpointManager | None = None
         if run_dir is not None:
             keep = int(cfg.trainer.extra.get("keep_last_k", 3))
-            self._ckpt_mgr = CheckpointManager(run_dir / "checkpoints", keep_last_k=keep)
+            # on GPU the write goes to a background thread behind a pinned-memory snapshot
+            # (trainer.extra.async_checkpoint, default on): the step pays the device-to-host copy only
+            async_ckpt = self._device.type == "cuda" and bool(cfg.trainer.extra.get("async_checkpoint", True))
+            self._ckpt_mgr = CheckpointManager(run_dir / "checkpoints", keep_last_k=keep, async_write=async_ckpt)
         self._run_dir = run_dir
         self.last_grad_norm: torch.Tensor | None = None
         logger.info(
@@ -404,6 +408,22 @@ class Trainer:
         max_steps_override: int | None = None,
         resume_from: str | Path | None = None,
     ) -> TrainResult:
+        """Train to ``max_steps``; an asynchronous checkpoint still being written is flushed to disk
+        before this returns or re-raises (a crash mid-run keeps the last complete checkpoint)."""
+        try:
+            result = self._fit(max_steps_override=max_steps_override, resume_from=resume_from)
+        except BaseException:
+            if self._ckpt_mgr is not None:
+                try:
+                    self._ckpt_mgr.wait()
+                except Exception:  # the training error is the one to report
+                    logger.exception("checkpoint: background write failed")
+            raise
+        if self._ckpt_mgr is not None:
+            self._ckpt_mgr.wait()
+        return result
+
+    def _fit(self, *, max_steps_override: int | None, resume_from: str | Path | None) -> TrainResult:
         cfg = self._cfg.trainer
         self._model.train()
         max_steps = max_steps_override if max_steps_override is not None else cfg.max_steps

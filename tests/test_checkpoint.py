@@ -108,3 +108,76 @@ def test_config_mismatch_warns(tmp_path: Path, trainer_records) -> None:  # type
     other = _cfg(tmp_path, max_steps=3, lr=1e-3)
     Trainer(other).fit(resume_from=str(tmp_path / "run" / "checkpoints"))
     assert any("config mismatch" in r.getMessage() for r in trainer_records)
+
+
+def test_async_writer_matches_sync_and_flushes(tmp_path) -> None:
+    """The background writer produces the same file contents as the synchronous path, keeps the
+    tied-weight aliasing, writes atomically, prunes, and wait() re-raises a write error."""
+    import torch
+
+    from llmtrain.training.checkpoint import CheckpointManager
+
+    class _Sched:
+        def state_dict(self):
+            return {"last_epoch": 3}
+
+    class _Cfg:
+        def model_dump(self):
+            return {"x": 1}
+
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(4, 4), torch.nn.Linear(4, 4))
+    model[1].weight = model[0].weight  # tied, like lm_head / token_embedding
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+    model(torch.randn(2, 4)).sum().backward()
+    opt.step()
+    sync = CheckpointManager(tmp_path / "sync", keep_last_k=1)
+    asyn = CheckpointManager(tmp_path / "async", keep_last_k=1, async_write=True)
+    for step in (1, 2):
+        sync.save(step, model, opt, _Sched(), _Cfg())
+        asyn.save(step, model, opt, _Sched(), _Cfg())
+    asyn.wait()
+    assert [p.name for p in asyn.checkpoints()] == ["step_000002.pt"]
+    assert not list((tmp_path / "async").glob("*.tmp"))
+    a, b = sync.load(sync.latest_checkpoint()), asyn.load(asyn.latest_checkpoint())
+    for k, v in a["model_state_dict"].items():
+        assert torch.equal(v, b["model_state_dict"][k])
+    sd = b["model_state_dict"]
+    assert sd["0.weight"].untyped_storage().data_ptr() == sd["1.weight"].untyped_storage().data_ptr()
+    assert a["optimizer_state_dict"]["state"][0]["step"] == b["optimizer_state_dict"]["state"][0]["step"]
+
+    bad = CheckpointManager(tmp_path / "bad", async_write=True)
+    bad._write = lambda payload, path: (_ for _ in ()).throw(OSError("disk full"))  # type: ignore[method-assign]
+    bad.save(1, model, opt, _Sched(), _Cfg())
+    try:
+        bad.wait()
+    except OSError as exc:
+        assert "disk full" in str(exc)
+    else:
+        raise AssertionError("wait() must re-raise the background write error")
+
+
+def test_async_snapshot_is_taken_at_save_time(tmp_path) -> None:
+    """Parameters changed right after save() (the next optimizer step) do not leak into the file
+    the background thread is still writing."""
+    import torch
+
+    from llmtrain.training.checkpoint import CheckpointManager
+
+    class _Sched:
+        def state_dict(self):
+            return {}
+
+    class _Cfg:
+        def model_dump(self):
+            return {}
+
+    model = torch.nn.Linear(8, 8)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    before = model.weight.detach().clone()
+    mgr = CheckpointManager(tmp_path, async_write=True)
+    mgr.save(1, model, opt, _Sched(), _Cfg())
+    with torch.no_grad():
+        model.weight.add_(1.0)
+    mgr.wait()
+    assert torch.equal(mgr.load(mgr.latest_checkpoint())["model_state_dict"]["weight"], before)

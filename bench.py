@@ -99,7 +99,7 @@ def make_config(args: argparse.Namespace, world: int):
             "max_grad_norm": 1.0,
             "extra": {"bucket_cap_mb": args.bucket_mb, "grad_reduce_dtype": args.grad_reduce_dtype},
         },
-        "ddp": {"enabled": world > 1, "backend": "nccl" if gpu else "gloo"},
+        "ddp": {"enabled": world > 1, "backend": getattr(args, "backend", "nccl") if gpu else "gloo"},
         "mlflow": {"enabled": False},
         "logging": {"log_to_file": False},
         "output": {"root_dir": "/tmp/llmtrain_bench_runs"},
@@ -122,6 +122,8 @@ def main() -> int:
     ap.add_argument("--dropout", type=float, default=0.0, help="model dropout (reference default 0.1)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda", help="cpu: contract tests only")
     ap.add_argument("--deterministic", action="store_true", help="fixed-order reductions (run.deterministic)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="gloo on GPU: rehearse the N-rank path on a box with fewer GPUs (ranks share devices)")
     args = ap.parse_args()
 
     if args.gpus < 1:
@@ -142,7 +144,7 @@ def main() -> int:
     if world > 1:
         ddp_state = setup_ddp(cfg)
         got_world, backend = dist.get_world_size(), dist.get_backend()
-        want_backend = "nccl" if gpu else "gloo"
+        want_backend = args.backend if gpu else "gloo"
         if got_world != args.gpus or backend != want_backend:
             raise RuntimeError(f"rank {ddp_state.rank}: world={got_world} backend={backend}, "
                                f"expected world={args.gpus} backend={want_backend}")

@@ -89,9 +89,13 @@ def setup_ddp(cfg: RunConfig) -> DDPState:
     backend = resolve_backend(cfg)
     kwargs = {}
     if _uses_gpu(cfg) and torch.cuda.is_available():
-        torch.cuda.set_device(local)
+        # local_rank modulo the visible devices, as runtime/device.py picks the device: identity on a
+        # full node; on a box with fewer GPUs than ranks (a gloo rehearsal of the multi-rank path)
+        # ranks share devices — RCCL itself refuses two ranks on one device
+        dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
         if backend == "nccl":
-            kwargs["device_id"] = torch.device("cuda", local)
+            kwargs["device_id"] = torch.device("cuda", dev)
     logger.info(
         "Initialising DDP process group: rank=%d, world_size=%d, local_rank=%d, backend=%s, "
         "init_method=env://",

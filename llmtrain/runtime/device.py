@@ -17,7 +17,7 @@ import torch
 
 from llmtrain.config.schemas import RunConfig
 
-__all__ = ["RuntimePolicy", "decorrelate_rank_streams", "resolve_policy", "seed_everything"]
+__all__ = ["RuntimePolicy", "decorrelate_rank_streams", "resolve_policy", "seed_everything", "settle_fused_path"]
 
 
 @dataclass(frozen=True)
@@ -81,3 +81,24 @@ def decorrelate_rank_streams(rank: int) -> int:
     if torch.cuda.is_available():
         torch.cuda.manual_seed_all(seed)
     return seed
+
+
+def settle_fused_path(policy: RuntimePolicy, cfg: RunConfig, supported: bool) -> RuntimePolicy:
+    """The fused engine was chosen but does not cover this model shape on ``policy.device``.
+
+    On the GPU the module path (torch SDPA + autograd + torch AdamW) is not a production backend:
+    an uncovered shape is an error unless the config opts in with
+    ``model.extra.allow_module_fallback: true`` (or asks for the module path with
+    ``model.extra.fused: false``).  On CPU the module path is the reference numerics and is taken
+    silently.
+    """
+    if not policy.use_fused or supported:
+        return policy
+    if policy.device.type == "cuda" and not cfg.model.extra.get("allow_module_fallback", False):
+        raise ValueError(
+            f"the fused MI355X engine does not cover this model shape (d_model={cfg.model.d_model}, "
+            f"n_heads={cfg.model.n_heads}, d_ff={cfg.model.d_ff}: head dims must be multiples of 8 up to 64, "
+            "or 128; d_model % 4 == 0 and <= 2048; d_ff % 8 == 0); set model.extra.allow_module_fallback: true "
+            "to train on the plain PyTorch module path instead, or model.extra.fused: false"
+        )
+    return RuntimePolicy(device=policy.device, compute_dtype=policy.compute_dtype, use_fused=False)

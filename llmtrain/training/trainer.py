@@ -28,7 +28,6 @@ What changes on the MI355X path:
 from __future__ import annotations
 
 import contextlib
-import dataclasses
 import logging
 import math
 import time
@@ -47,7 +46,7 @@ from llmtrain.parallel.dist import DDPState
 from llmtrain.registry import initialize_registries
 from llmtrain.registry.data import get_data_module
 from llmtrain.registry.models import get_model_adapter
-from llmtrain.runtime.device import decorrelate_rank_streams, resolve_policy, seed_everything
+from llmtrain.runtime.device import decorrelate_rank_streams, resolve_policy, seed_everything, settle_fused_path
 from llmtrain.runtime.tuning import enable_tuned_gemms
 from llmtrain.tracking import NullTracker, Tracker
 from llmtrain.training.checkpoint import CheckpointManager, CheckpointPayload, restore_rng_states
@@ -171,9 +170,10 @@ class Trainer:
         fused_capable = hasattr(model, "prepare_runtime") and supported is not None
         policy = resolve_policy(cfg, local_rank=local_rank, fused_capable=fused_capable)
         if policy.use_fused and not supported(policy.device.type):
+            # an error on GPU unless model.extra.allow_module_fallback (runtime/device.py)
+            policy = settle_fused_path(policy, cfg, False)
             logger.warning("trainer: fused engine does not cover this model shape on %s; using the module path",
                            policy.device)
-            policy = dataclasses.replace(policy, use_fused=False)
         self._policy = policy
         self._device = self._policy.device
         self.tuned_gemms = enable_tuned_gemms(self._device)  # shipped hipBLASLt solution table (GPU)

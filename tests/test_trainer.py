@@ -126,3 +126,29 @@ def test_fault_injection_fires_once_then_resume_completes(tmp_path) -> None:  # 
     restart.mkdir()
     result = Trainer(cfg, run_dir=restart).fit(resume_from=str(run / "checkpoints"))
     assert result.resumed_from_step == 4 and result.final_step == 6
+
+
+def test_gpu_shape_fallback_is_opt_in() -> None:
+    """On the GPU an uncovered model shape is an error unless the config opts into the module path;
+    on CPU the module path is taken silently (runtime/device.py settle_fused_path)."""
+    import pytest
+    import torch
+
+    from llmtrain.config.schemas import RunConfig
+    from llmtrain.runtime.device import RuntimePolicy, settle_fused_path
+
+    import yaml
+
+    base = yaml.safe_load(open("configs/presets/gpt_smoke.yaml"))
+
+    def cfg(extra):
+        payload = dict(base, model=dict(base["model"], extra=extra))
+        return RunConfig.model_validate(payload)
+
+    gpu = RuntimePolicy(device=torch.device("cuda", 0), compute_dtype=torch.bfloat16, use_fused=True)
+    with pytest.raises(ValueError, match="allow_module_fallback"):
+        settle_fused_path(gpu, cfg({}), supported=False)
+    assert not settle_fused_path(gpu, cfg({"allow_module_fallback": True}), supported=False).use_fused
+    assert settle_fused_path(gpu, cfg({}), supported=True).use_fused
+    cpu = RuntimePolicy(device=torch.device("cpu"), compute_dtype=torch.float32, use_fused=True)
+    assert not settle_fused_path(cpu, cfg({}), supported=False).use_fused

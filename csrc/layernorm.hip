@@ -284,6 +284,148 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 }
 
+// Lean backward for rows of <= 768 columns.  Same math as ln_bwd_kernel, built for latency
+// hiding rather than for the fewest instructions:
+//  * every load is unconditional (lanes past the row end read column 0 and are zeroed): a load
+//    under a divergent `if` gets its own vmcnt(0) at the branch join, which serialised each row
+//    into one HBM round trip per 256-column chunk in the prefetching kernel;
+//  * ROWS rows per wave per iteration, all their loads issued before the first reduction;
+//  * the dproj column partial in this wave's own LDS row instead of registers (12 KB per
+//    workgroup; per-wave rows keep the summation order fixed, i.e. deterministic), gamma re-read
+//    from L1 at each use.
+// The side stream's weight-gradient GEMM (wgrad_kernel<4,4>: 74 VGPRs + 256 AGPRs = 336 of a
+// SIMD's 512) leaves 176 registers per SIMD, so what LayerNorm backward has in flight on the CUs
+// that GEMM holds is bounded by load-destination registers, not by wave count.
+template <int MAXC, int ROWS, typename TDY, bool LOWP_OUT>
+__global__ __launch_bounds__(256, ROWS == 1 ? 4 : 3) void ln_bwd_lean_kernel(
+    const TDY* __restrict__ dy, const float* __restrict__ xs, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const float* __restrict__ w, const float* __restrict__ dresid,
+    const float* __restrict__ dy_scale, float* __restrict__ dx, TDY* __restrict__ dx_lp,
+    float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dproj, int M, int d, DropoutArgs dr) {
+  static_assert(MAXC <= 3, "lean LayerNorm backward is for rows of <= 768 columns");
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // [kBwdWaves][d]
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nc = d >> 2;
+  const float scale = dy_scale != nullptr ? *dy_scale : 1.f;
+  const float inv_d = 1.f / (float)d;
+  const bool has_pp = dproj != nullptr;
+  const float4_t zero = {0.f, 0.f, 0.f, 0.f};
+  float* pp = smem + wid * d;  // this wave's dproj column partial
+
+  float4_t pw[MAXC], pb[MAXC];
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    pw[j] = zero; pb[j] = zero;
+    const int c = lane + j * 64;
+    if (has_pp && c < nc) store4(pp + 4 * c, zero);
+  }
+
+  const long stride = (long)gridDim.x * kBwdWaves;
+  for (long row0 = (long)blockIdx.x * kBwdWaves + wid; row0 < M; row0 += ROWS * stride) {
+    // gamma through a row-dependent (always zero) offset: keeps the compiler from hoisting the
+    // loop-invariant loads into 12 live registers
+    const float* wr = w + __builtin_amdgcn_readfirstlane((int)(row0 >> 40));
+    long rows[ROWS];
+    bool live[ROWS];
+    float mu[ROWS], rs[ROWS];
+    float4_t g[ROWS][MAXC], xh[ROWS][MAXC], rr[ROWS][MAXC];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+      live[r] = row0 + r * stride < M;  // wave-uniform
+      rows[r] = live[r] ? row0 + r * stride : row0;
+      mu[r] = mean[rows[r]];
+      rs[r] = rstd[rows[r]];
+#pragma unroll
+      for (int j = 0; j < MAXC; ++j) {
+        const int c = lane + j * 64, cc = c < nc ? c : 0;
+        g[r][j] = load4(dy + rows[r] * d + 4 * cc);
+        xh[r][j] = load4_nt(xs + rows[r] * d + 4 * cc);
+      }
+    }
+    if (dresid != nullptr) {
+#pragma unroll
+      for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+        for (int j = 0; j < MAXC; ++j) {
+          const int c = lane + j * 64, cc = c < nc ? c : 0;
+          rr[r][j] = load4_nt(dresid + rows[r] * d + 4 * cc);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < MAXC; ++j) {
+        const int c = lane + j * 64, cc = c < nc ? c : 0;
+        const bool ok = live[r] && c < nc;
+        g[r][j] = ok ? g[r][j] * scale : zero;
+        xh[r][j] = ok ? (xh[r][j] - mu[r]) * rs[r] : zero;
+        float4_t gw = g[r][j] * load4(wr + 4 * cc);
+        s1 += gw[0] + gw[1] + gw[2] + gw[3];
+        float4_t gx = gw * xh[r][j];
+        s2 += gx[0] + gx[1] + gx[2] + gx[3];
+      }
+      const float c1 = wave_sum(s1) * inv_d, c2 = wave_sum(s2) * inv_d;
+      const long row = rows[r];
+#pragma unroll
+      for (int j = 0; j < MAXC; ++j) {
+        const int c = lane + j * 64, cc = c < nc ? c : 0;
+        float4_t out = (g[r][j] * load4(wr + 4 * cc) - c1 - xh[r][j] * c2) * rs[r];
+        if (dresid != nullptr) out += rr[r][j];
+        float4_t br = out;
+        if (dr.thr != 0) {
+          const uint64_t e0 = (uint64_t)row * d + 4 * c;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) br[t] = drop_keep(dr.seed, dr.thr, e0 + t) ? out[t] * dr.scale : 0.f;
+        }
+        pw[j] += g[r][j] * xh[r][j];  // zero past the row end and for a dead row
+        pb[j] += g[r][j];
+        if (live[r] && c < nc) {
+          store4_nt(dx + row * d + 4 * c, out);
+          if (LOWP_OUT) store4(dx_lp + row * d + 4 * c, br);
+          if (has_pp) store4(pp + 4 * c, *reinterpret_cast<const float4_t*>(pp + 4 * c) + br);
+        }
+      }
+    }
+  }
+
+  // dproj partials are already in LDS: reduce them first, then dw and db through the same buffer
+  const int nacc = has_pp ? 3 : 2;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (k >= nacc) break;
+    const int which = has_pp ? (k == 0 ? 2 : k - 1) : k;
+    if (which != 2) {  // dw / db: stage this wave's register partial (dproj is already there)
+      if (k > 0) __syncthreads();  // previous round's readers are done with the buffer
+#pragma unroll
+      for (int j = 0; j < MAXC; ++j) {
+        const int c = lane + j * 64;
+        if (c < nc) store4(smem + wid * d + 4 * c, which == 0 ? pw[j] : pb[j]);
+      }
+    }
+    __syncthreads();
+    float* dst = which == 0 ? dw : (which == 1 ? db : dproj);
+    for (int col = threadIdx.x; col < d; col += blockDim.x) {
+      float acc = 0.f;
+#pragma unroll
+      for (int wv2 = 0; wv2 < kBwdWaves; ++wv2) acc += smem[wv2 * d + col];
+      dst[(long)blockIdx.x * d + col] = acc;
+    }
+  }
+}
+
+// LLMT_LN_BWD_LEAN: rows per wave per iteration of the lean kernel (1 or 2; default 1) for rows of
+// <= 768 columns; 0 = the prefetching kernel
+inline int ln_bwd_lean_rows(int maxc) {
+  static const int rows = [] {
+    const char* e = std::getenv("LLMT_LN_BWD_LEAN");
+    const int v = e ? std::atoi(e) : 1;
+    return v < 0 ? 0 : (v > 2 ? 2 : v);
+  }();
+  return maxc <= 3 ? rows : 0;
+}
+inline bool ln_bwd_lean(int maxc) { return ln_bwd_lean_rows(maxc) > 0; }
+
 template <int MAXC>
 void launch_fwd_c(const LnFwdArgs& a, hipStream_t st) {
   dim3 grid((a.M + kLnWaves - 1) / kLnWaves), block(256);
@@ -299,6 +441,17 @@ void launch_fwd_c(const LnFwdArgs& a, hipStream_t st) {
 #undef LN_FWD
 }
 
+// The backward kernel for this row width and LLMT_LN_BWD_LEAN setting (one signature for all)
+template <int MAXC, typename TDY, bool LP>
+auto bwd_kernel() -> decltype(&ln_bwd_kernel<MAXC, TDY, LP>) {
+  constexpr int LC = MAXC < 3 ? MAXC : 3;
+  switch (ln_bwd_lean_rows(MAXC)) {
+    case 1: return &ln_bwd_lean_kernel<LC, 1, TDY, LP>;
+    case 2: return &ln_bwd_lean_kernel<LC, 2, TDY, LP>;
+    default: return &ln_bwd_kernel<MAXC, TDY, LP>;
+  }
+}
+
 template <int MAXC>
 int bwd_grid_c(const LnBwdArgs& a) {
   const size_t shm = (size_t)kBwdWaves * a.d * sizeof(float);
@@ -310,19 +463,21 @@ int bwd_grid_c(const LnBwdArgs& a) {
     int n = 0, dev = 0, cus = 0;
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const bool lean = ln_bwd_lean(MAXC);
     if (a.dy_bf16)
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, a.dx_lp ? ln_bwd_kernel<MAXC, bf16_raw, true>
-                                                              : ln_bwd_kernel<MAXC, bf16_raw, false>, 256, shm);
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, a.dx_lp ? bwd_kernel<MAXC, bf16_raw, true>()
+                                                              : bwd_kernel<MAXC, bf16_raw, false>(), 256, shm);
     else
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, a.dx_lp ? ln_bwd_kernel<MAXC, float, true>
-                                                              : ln_bwd_kernel<MAXC, float, false>, 256, shm);
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, a.dx_lp ? bwd_kernel<MAXC, float, true>()
+                                                              : bwd_kernel<MAXC, float, false>(), 256, shm);
     // LLMT_LN_BWD_WAVES: resident waves of workgroups per launch (A/B knob; default 4 for rows of <= 768
     // columns, 1 above: GPT-2 XL d = 1600 measured 80.0k (1) vs 79.7k (4) tok/s).  More
     // than one lets the hardware dispatcher balance rows onto CUs the side stream's weight-
     // gradient GEMMs free up (124M / micro-batch 128 same-box: 1 -> 1.0224M, 2 -> 1.0259M,
-    // 4 -> 1.0276M, 8 -> 1.0243M tok/s).
+    // 4 -> 1.0276M, 8 -> 1.0243M tok/s).  The lean kernel: 3 (about the same workgroup count and
+    // column-partial traffic as 4 of the prefetching one).
     const char* e = std::getenv("LLMT_LN_BWD_WAVES");
-    const int waves = e ? std::max(1, std::atoi(e)) : (MAXC <= 3 ? 4 : 1);
+    const int waves = e ? std::max(1, std::atoi(e)) : (lean ? 3 : (MAXC <= 3 ? 4 : 1));
     per_cu = (n > 0 ? n : 4) * (cus > 0 ? cus : 256) * waves;
   }
   return stride_grid((long long)(a.M + kBwdWaves - 1) / kBwdWaves, 1, per_cu);
@@ -335,16 +490,20 @@ void launch_bwd_c(const LnBwdArgs& a, hipStream_t st) {
   float* pw = a.ws;
   float* pb = a.ws + (long)grid * a.d;
   float* pp = a.dproj != nullptr ? a.ws + 2L * grid * a.d : nullptr;
-#define LN_BWD(TDY, LP)                                                                         \
-  hipLaunchKernelGGL((ln_bwd_kernel<MAXC, TDY, LP>), dim3(grid), dim3(256), shm, st,            \
-                     (const TDY*)a.dy, a.xs, a.mean, a.rstd, a.w, a.dresid, a.dy_scale, a.dx,    \
-                     (TDY*)a.dx_lp, pw, pb, pp, a.M, a.d, a.dropout)
-  if (a.dy_bf16) {
-    if (a.dx_lp != nullptr) LN_BWD(bf16_raw, true); else LN_BWD(bf16_raw, false);
-  } else {
-    if (a.dx_lp != nullptr) LN_BWD(float, true); else LN_BWD(float, false);
-  }
-#undef LN_BWD
+  const void* fn = nullptr;
+  if (a.dy_bf16)
+    fn = (const void*)(a.dx_lp != nullptr ? bwd_kernel<MAXC, bf16_raw, true>() : bwd_kernel<MAXC, bf16_raw, false>());
+  else
+    fn = (const void*)(a.dx_lp != nullptr ? bwd_kernel<MAXC, float, true>() : bwd_kernel<MAXC, float, false>());
+  const void* dy = a.dy;
+  void* dx_lp = a.dx_lp;
+  const float *xs = a.xs, *mean = a.mean, *rstd = a.rstd, *w = a.w, *dresid = a.dresid, *dy_scale = a.dy_scale;
+  float* dx = a.dx;
+  int M = a.M, d = a.d;
+  DropoutArgs dr = a.dropout;
+  void* args[] = {&dy, &xs, &mean, &rstd, &w, &dresid, &dy_scale, &dx, &dx_lp, &pw, &pb, &pp, &M, &d, &dr};
+  (void)hipLaunchKernel(fn, dim3(grid), dim3(256), args, shm, st);
+
   const int nacc = a.dproj != nullptr ? 3 : 2;
   float* scratch = a.ws + (long)nacc * grid * a.d;
   const float* parts[3] = {pw, pb, pp};

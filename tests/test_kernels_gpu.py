@@ -43,8 +43,12 @@ def test_add_layernorm_fwd(gpu_device, M, d, with_delta):
     _close(y, y_r, 2e-2, 1e-2, "y(bf16)")
 
 
-@pytest.mark.parametrize("M,d", [(4096, 768), (100, 64)])
-def test_layernorm_bwd(gpu_device, M, d):
+@pytest.mark.parametrize("M,d", [(4096, 768), (4099, 768), (100, 64), (777, 384), (513, 1600)])
+@pytest.mark.parametrize("with_proj,lowp", [(True, True), (False, False), (False, True)])
+def test_layernorm_bwd(gpu_device, M, d, with_proj, lowp):
+    """Every LayerNorm-backward variant (LLMT_LN_BWD_LEAN picks the kernel for d <= 768; the
+    GPU tier is also run under each setting) against the fp32 reference: with / without the
+    projection-bias column sum and the bf16 copy, odd row counts (dead rows of a 2-row wave)."""
     g = torch.Generator(device="cpu").manual_seed(7)
     x = torch.randn(M, d, generator=g).to(gpu_device)
     w = (1 + 0.1 * torch.randn(d, generator=g)).to(gpu_device)
@@ -55,14 +59,18 @@ def test_layernorm_bwd(gpu_device, M, d):
     scale = torch.tensor(0.5, device=gpu_device)
     dw, db, dp = (torch.full((d,), 0.25, device=gpu_device) for _ in range(3))
     dw_r, db_r, dp_r = dw.clone(), db.clone(), dp.clone()
-    dx, dx_lp = hip().layernorm_bwd(dy, x, mu, rs, w, dres, dw, db, scale, True, dp)
+    dx, dx_lp = hip().layernorm_bwd(dy, x, mu, rs, w, dres, dw, db, scale, lowp, dp if with_proj else None)
     dx_r = ref.layernorm_bwd(dy, x, mu, rs, w, dres, dw_r, db_r, scale)
     ref.colsum_accum(dx_r, dp_r)
     _close(dx, dx_r, 1e-4, 1e-4, "dx")
-    _close(dx_lp, dx_r, 2e-2, 1e-2, "dx_lp")
+    if lowp:
+        _close(dx_lp, dx_r, 2e-2, 1e-2, "dx_lp")
     _close(dw, dw_r, 1e-2, 1e-4, "dgamma")
     _close(db, db_r, 1e-2, 1e-4, "dbeta")
-    _close(dp, dp_r, 2e-2, 1e-4, "dproj")
+    if with_proj:
+        _close(dp, dp_r, 2e-2, 1e-4, "dproj")
+    else:
+        assert torch.equal(dp, torch.full((d,), 0.25, device=gpu_device))
 
 
 @pytest.mark.parametrize("M,V,Vp", [(256, 50257, 50304), (64, 16, 64), (33, 1000, 1024)])

@@ -57,25 +57,40 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
   if (row >= M) return;
   const int nc = d >> 2;
   const float* xr = x + row * d;
-  float4_t v[MAXC];
+  // unconditional loads (lanes past the row end read column 0 and are zeroed): a load under a
+  // divergent `if` gets a vmcnt(0) at the branch join, one HBM round trip per 256-column chunk
+  // gamma / beta are loaded with the row (on gfx950 vmcnt also counts stores: loading them after
+  // the xs stores would wait for those stores to complete)
+  float4_t v[MAXC], dv[MAXC], ww[MAXC], bb[MAXC];
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int c = lane + j * 64, cc = c < nc ? c : 0;
+    v[j] = load4(xr + 4 * cc);
+    ww[j] = load4(w + 4 * cc);
+    bb[j] = load4(b + 4 * cc);
+  }
+  if (delta != nullptr) {
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = lane + j * 64, cc = c < nc ? c : 0;
+      dv[j] = load4(delta + row * d + 4 * cc);
+    }
+  }
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < MAXC; ++j) {
     const int c = lane + j * 64;
-    if (c < nc) {
-      v[j] = load4(xr + 4 * c);
-      if (delta != nullptr) {
-        float4_t dv = load4(delta + row * d + 4 * c);
-        if (dr.thr != 0) {  // residual-branch dropout (reference gpt.py resid/mlp_dropout)
-          const uint64_t e0 = (uint64_t)row * d + 4 * c;
+    if (delta != nullptr) {
+      if (dr.thr != 0) {  // residual-branch dropout (reference gpt.py resid/mlp_dropout)
+        const uint64_t e0 = (uint64_t)row * d + 4 * c;
 #pragma unroll
-          for (int t = 0; t < 4; ++t) dv[t] = drop_keep(dr.seed, dr.thr, e0 + t) ? dv[t] * dr.scale : 0.f;
-        }
-        v[j] += dv;
-        store4(xs_out + row * d + 4 * c, v[j]);
+        for (int t = 0; t < 4; ++t) dv[j][t] = drop_keep(dr.seed, dr.thr, e0 + t) ? dv[j][t] * dr.scale : 0.f;
       }
-      s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
+      v[j] += dv[j];
+      if (c < nc) store4(xs_out + row * d + 4 * c, v[j]);
     }
+    if (c >= nc) v[j] = float4_t{0.f, 0.f, 0.f, 0.f};
+    s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
   }
   const float inv_d = 1.f / (float)d;
   const float mu = wave_sum(s) * inv_d;
@@ -92,10 +107,8 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
 #pragma unroll
   for (int j = 0; j < MAXC; ++j) {
     const int c = lane + j * 64;
-    if (c < nc) {
-      float4_t ww = load4(w + 4 * c), bb = load4(b + 4 * c);
-      store4(y + row * d + 4 * c, (v[j] - mu) * rs * ww + bb);
-    }
+    const float4_t out = (v[j] - mu) * rs * ww[j] + bb[j];
+    if (c < nc) store4(y + row * d + 4 * c, out);
   }
   if (lane == 0) {
     mean_out[row] = mu;
@@ -284,7 +297,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 }
 
-// Lean backward for rows of <= 768 columns.  Same math as ln_bwd_kernel, built for latency
+// Lean backward (every row width).  Same math as ln_bwd_kernel, built for latency
 // hiding rather than for the fewest instructions:
 //  * every load is unconditional (lanes past the row end read column 0 and are zeroed): a load
 //    under a divergent `if` gets its own vmcnt(0) at the branch join, which serialised each row
@@ -297,12 +310,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 // SIMD's 512) leaves 176 registers per SIMD, so what LayerNorm backward has in flight on the CUs
 // that GEMM holds is bounded by load-destination registers, not by wave count.
 template <int MAXC, int ROWS, typename TDY, bool LOWP_OUT>
-__global__ __launch_bounds__(256, ROWS == 1 ? 4 : 3) void ln_bwd_lean_kernel(
+__global__ __launch_bounds__(256, ROWS == 1 ? (MAXC <= 3 ? 4 : 2) : 3) void ln_bwd_lean_kernel(
     const TDY* __restrict__ dy, const float* __restrict__ xs, const float* __restrict__ mean,
     const float* __restrict__ rstd, const float* __restrict__ w, const float* __restrict__ dresid,
     const float* __restrict__ dy_scale, float* __restrict__ dx, TDY* __restrict__ dx_lp,
     float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dproj, int M, int d, DropoutArgs dr) {
-  static_assert(MAXC <= 3, "lean LayerNorm backward is for rows of <= 768 columns");
   extern __shared__ __attribute__((aligned(16))) float smem[];  // [kBwdWaves][d]
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nc = d >> 2;
@@ -414,15 +426,20 @@ __global__ __launch_bounds__(256, ROWS == 1 ? 4 : 3) void ln_bwd_lean_kernel(
   }
 }
 
-// LLMT_LN_BWD_LEAN: rows per wave per iteration of the lean kernel (1 or 2; default 1) for rows of
-// <= 768 columns; 0 = the prefetching kernel
+// LLMT_LN_BWD_LEAN: rows per wave per iteration of the lean kernel (1, or 2 for rows of <= 768
+// columns; default 1); 0 = the prefetching kernel.  LLMT_LN_BWD_LEAN_WIDE=0 keeps the prefetching
+// kernel for rows wider than 768 columns (GPT-2 XL's 1600).
 inline int ln_bwd_lean_rows(int maxc) {
   static const int rows = [] {
     const char* e = std::getenv("LLMT_LN_BWD_LEAN");
     const int v = e ? std::atoi(e) : 1;
     return v < 0 ? 0 : (v > 2 ? 2 : v);
   }();
-  return maxc <= 3 ? rows : 0;
+  static const bool wide = [] {
+    const char* e = std::getenv("LLMT_LN_BWD_LEAN_WIDE");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return (maxc <= 3 || wide) ? rows : 0;
 }
 inline bool ln_bwd_lean(int maxc) { return ln_bwd_lean_rows(maxc) > 0; }
 
@@ -444,10 +461,9 @@ void launch_fwd_c(const LnFwdArgs& a, hipStream_t st) {
 // The backward kernel for this row width and LLMT_LN_BWD_LEAN setting (one signature for all)
 template <int MAXC, typename TDY, bool LP>
 auto bwd_kernel() -> decltype(&ln_bwd_kernel<MAXC, TDY, LP>) {
-  constexpr int LC = MAXC < 3 ? MAXC : 3;
   switch (ln_bwd_lean_rows(MAXC)) {
-    case 1: return &ln_bwd_lean_kernel<LC, 1, TDY, LP>;
-    case 2: return &ln_bwd_lean_kernel<LC, 2, TDY, LP>;
+    case 1: return &ln_bwd_lean_kernel<MAXC, 1, TDY, LP>;
+    case 2: return &ln_bwd_lean_kernel<MAXC, MAXC <= 3 ? 2 : 1, TDY, LP>;
     default: return &ln_bwd_kernel<MAXC, TDY, LP>;
   }
 }
@@ -477,7 +493,7 @@ int bwd_grid_c(const LnBwdArgs& a) {
     // 4 -> 1.0276M, 8 -> 1.0243M tok/s).  The lean kernel: 3 (about the same workgroup count and
     // column-partial traffic as 4 of the prefetching one).
     const char* e = std::getenv("LLMT_LN_BWD_WAVES");
-    const int waves = e ? std::max(1, std::atoi(e)) : (lean ? 3 : (MAXC <= 3 ? 4 : 1));
+    const int waves = e ? std::max(1, std::atoi(e)) : (MAXC <= 3 ? (lean ? 3 : 4) : 1);
     per_cu = (n > 0 ? n : 4) * (cus > 0 ? cus : 256) * waves;
   }
   return stride_grid((long long)(a.M + kBwdWaves - 1) / kBwdWaves, 1, per_cu);

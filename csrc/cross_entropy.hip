@@ -8,6 +8,8 @@
 //     dlogits = (softmax(z) - onehot(label)) * row_weight[row]      (0 for padded columns)
 // so the backward never touches the logits as logits again.  At GPT-2 vocab this is one read
 // and one write of 100 KB per row, i.e. HBM-bound at ~2 * M * Vp * 2 bytes.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -62,8 +64,10 @@ struct Vec8<float> {
   }
 };
 
-template <int MAXV, typename T>
-__global__ __launch_bounds__(kCeThreads, 6) void ce_fwd_bwd_kernel(
+// OCC: waves per SIMD the register budget is sized for (6 = 3 rows per CU at 80 VGPRs; 5 = 2 rows
+// per CU at 96, no spill of the row's last vector now that all of a row's loads are in flight)
+template <int MAXV, typename T, int OCC = 6>
+__global__ __launch_bounds__(kCeThreads, OCC) void ce_fwd_bwd_kernel(
     T* __restrict__ logits, const int64_t* __restrict__ labels, const float* __restrict__ row_w,
     float* __restrict__ loss, int Vp, int V) {
   __shared__ float scratch[kCeWaves];
@@ -73,18 +77,27 @@ __global__ __launch_bounds__(kCeThreads, 6) void ce_fwd_bwd_kernel(
   const int64_t label = labels[row];
   LLMT_DASSERT(label < V);  // negative = ignored row; >= V is a data bug
   const bool valid = label >= 0 && label < V;
-  const float t_label = valid ? scalar_f(z[label]) * kLog2e : 0.f;  // read before any write
+
+  // Every vector load of the row is issued before the first wait: the loads are unconditional
+  // (vectors past the row end re-read vector 0 and are ignored below) — a load under a divergent
+  // `if` gets its own vmcnt(0) at the branch join, which had serialised the row into 13 HBM
+  // round trips per thread.  The label logit is read with them (before any write).
+  Vec8<T> v[MAXV];
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = threadIdx.x + j * kCeThreads;
+    v[j].load(z + 8 * (c < nvec ? c : 0));
+  }
+  const float t_label = valid ? scalar_f(z[valid ? label : 0]) * kLog2e : 0.f;
 
   // Only the row's last vector can hold padded columns (Vp - V < 64) and only one vector holds
   // the label: both are handled per vector, so the per-element loops carry no compares.
   const int nfull = V >> 3;  // vectors with 8 real columns
-  Vec8<T> v[MAXV];
   float m = -INFINITY;
 #pragma unroll
   for (int j = 0; j < MAXV; ++j) {
     const int c = threadIdx.x + j * kCeThreads;
     if (c < nvec) {
-      v[j].load(z + 8 * c);
       if (c < nfull) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) m = fmaxf(m, v[j].get(i));
@@ -149,6 +162,15 @@ hipError_t launch_t(T* logits, const int64_t* labels, const float* row_w, float*
     hipLaunchKernelGGL((ce_fwd_bwd_kernel<N, T>), grid, block, 0, st, logits, labels, row_w, loss, \
                        Vp, V);                                                                   \
     break;
+  // LLMT_CE_OCC=5 (A/B): the 13-vector (GPT-2 vocabulary) kernel at 2 rows per CU
+  static const int occ = [] {
+    const char* e = std::getenv("LLMT_CE_OCC");
+    return e ? std::atoi(e) : 6;
+  }();
+  if (maxv == 13 && occ == 5) {
+    hipLaunchKernelGGL((ce_fwd_bwd_kernel<13, T, 5>), grid, block, 0, st, logits, labels, row_w, loss, Vp, V);
+    return hipGetLastError();
+  }
   switch (maxv) {
     CE_CASE(1) CE_CASE(2) CE_CASE(4) CE_CASE(8) CE_CASE(13) CE_CASE(16) CE_CASE(26) CE_CASE(32)
     default: {

@@ -269,6 +269,11 @@ def linear_dx_attn(dy, w, att, seqlen: int, v_bias_grad=None, head_dim: int = 64
     return torch.mm(dy, w), None
 
 
+# LLMTRAIN_WGRAD_SIDE_TILE (A/B): force the 128- or 256-wide tile for the weight gradients that share
+# the chip with the main stream (0 = the cost model's choice)
+_SIDE_WGRAD_TILE = int(os.environ.get("LLMTRAIN_WGRAD_SIDE_TILE", "0"))
+
+
 def wgrad_accum(dst, dy, x, *, exclusive: bool = False) -> None:
     """``dst (fp32 [N, K]) += dy[M, N]^T @ x[M, K]`` — split-K MFMA GEMM with atomic fp32
     accumulation on GPU (``dy`` may be a column slice with a larger row stride).  ``exclusive``:
@@ -277,7 +282,7 @@ def wgrad_accum(dst, dy, x, *, exclusive: bool = False) -> None:
     gradients keep the 332-register kernel so main-stream waves can share its CUs (with the
     pipelined one the fc-bias column sum behind them waited ~490 us per layer)."""
     if _on_gpu(dst):
-        hip_ops().wgrad_gemm(dy, x, dst, 0, 0, 4 if exclusive else 0)
+        hip_ops().wgrad_gemm(dy, x, dst, 0, 0 if exclusive else _SIDE_WGRAD_TILE, 4 if exclusive else 0)
     else:
         dst.addmm_(dy.t().float(), x.float())
 

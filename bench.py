@@ -43,8 +43,14 @@ MODELS = {
     "gpt2-124m": dict(vocab_size=50257, block_size=1024, d_model=768, n_layers=12, n_heads=12, d_ff=3072),
     "gpt2-xl": dict(vocab_size=50257, block_size=1024, d_model=1600, n_layers=48, n_heads=25, d_ff=6400),
     "tiny": dict(vocab_size=512, block_size=64, d_model=64, n_layers=2, n_heads=2, d_ff=128),  # CPU tests
+    # the reference presets' model shapes (configs/presets/*.yaml) with the GPT-2 vocabulary:
+    # launch-bound on an MI355X, the case --cuda-graph is for
+    "wikitext-better": dict(vocab_size=50257, block_size=256, d_model=384, n_layers=12, n_heads=8, d_ff=1536),
+    "wikitext-ddp": dict(vocab_size=50257, block_size=256, d_model=256, n_layers=4, n_heads=4, d_ff=1024),
 }
-MODEL_LABEL = {"gpt2-124m": "GPT-2 124M", "gpt2-xl": "GPT-2 XL 1.5B", "tiny": "tiny (CPU contract test)"}
+MODEL_LABEL = {"gpt2-124m": "GPT-2 124M", "gpt2-xl": "GPT-2 XL 1.5B", "tiny": "tiny (CPU contract test)",
+               "wikitext-better": "gpt_wikitext_better shape (d 384, 12 layers)",
+               "wikitext-ddp": "gpt_wikitext_ddp shape (d 256, 4 layers)"}
 
 
 def _free_port() -> int:
@@ -97,7 +103,8 @@ def make_config(args: argparse.Namespace, world: int):
             "weight_decay": 0.1,
             "warmup_steps": 0,
             "max_grad_norm": 1.0,
-            "extra": {"bucket_cap_mb": args.bucket_mb, "grad_reduce_dtype": args.grad_reduce_dtype},
+            "extra": {"bucket_cap_mb": args.bucket_mb, "grad_reduce_dtype": args.grad_reduce_dtype,
+                      "cuda_graph": bool(getattr(args, "cuda_graph", False))},
         },
         "ddp": {"enabled": world > 1, "backend": getattr(args, "backend", "nccl") if gpu else "gloo"},
         "mlflow": {"enabled": False},
@@ -122,6 +129,8 @@ def main() -> int:
     ap.add_argument("--dropout", type=float, default=0.0, help="model dropout (reference default 0.1)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda", help="cpu: contract tests only")
     ap.add_argument("--deterministic", action="store_true", help="fixed-order reductions (run.deterministic)")
+    ap.add_argument("--cuda-graph", action="store_true",
+                    help="capture the optimizer step as a hipGraph and replay it (1 GPU, dropout 0)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo on GPU: rehearse the N-rank path on a box with fewer GPUs (ranks share devices)")
     args = ap.parse_args()
@@ -222,6 +231,7 @@ def main() -> int:
                 "grad_reduce_dtype": args.grad_reduce_dtype,
                 "deterministic": args.deterministic,
                 "backend": dist.get_backend() if world > 1 else None,
+                "cuda_graph": bool(args.cuda_graph),
             },
             "tokens_per_sec_per_gpu": round(tps / world, 1),
             "per_rank_tokens_per_sec": [round(r[1] / r[0], 1) for r in rows],

@@ -31,8 +31,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ param, c
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     void* __restrict__ shadow,
                                                     const float* __restrict__ grad_scale, long n,
-                                                    AdamScalars s) {
+                                                    AdamScalars s, const float* __restrict__ dyn) {
   const float gs = grad_scale != nullptr ? *grad_scale : 1.f;
+  if (dyn != nullptr) {  // graph replay: this step's scalars from device memory
+    s.decay = dyn[0];
+    s.step_size = dyn[1];
+    s.bc2_sqrt = dyn[2];
+  }
   const long n4 = n >> 2;
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -100,23 +105,31 @@ __global__ __launch_bounds__(kSumsqThreads) void sumsq_final_kernel(const float*
 
 }  // namespace
 
+void adamw_step_scalars(const AdamWArgs& a, float out[3]) {
+  out[0] = 1.f - a.lr * a.weight_decay;
+  out[1] = a.lr / a.bias_correction1;
+  out[2] = a.bias_correction2_sqrt;
+}
+
 hipError_t launch_adamw_flat(const AdamWArgs& a, hipStream_t stream) {
   if (a.n <= 0) return hipSuccess;
+  float per_step[3];
+  adamw_step_scalars(a, per_step);
   AdamScalars s;
-  s.decay = 1.f - a.lr * a.weight_decay;
+  s.decay = per_step[0];
   s.one_minus_b1 = 1.f - a.beta1;
   s.b2 = a.beta2;
   s.one_minus_b2 = 1.f - a.beta2;
-  s.step_size = a.lr / a.bias_correction1;
-  s.bc2_sqrt = a.bias_correction2_sqrt;
+  s.step_size = per_step[1];
+  s.bc2_sqrt = per_step[2];
   s.eps = a.eps;
   const int grid = stride_grid((a.n + 3) / 4, 256, 256 * 8);
   if (a.shadow_bf16)
     hipLaunchKernelGGL(adamw_kernel<true>, dim3(grid), dim3(256), 0, stream, a.param, a.grad, a.exp_avg,
-                       a.exp_avg_sq, a.shadow, a.grad_scale, (long)a.n, s);
+                       a.exp_avg_sq, a.shadow, a.grad_scale, (long)a.n, s, a.dyn);
   else
     hipLaunchKernelGGL(adamw_kernel<false>, dim3(grid), dim3(256), 0, stream, a.param, a.grad, a.exp_avg,
-                       a.exp_avg_sq, a.shadow, a.grad_scale, (long)a.n, s);
+                       a.exp_avg_sq, a.shadow, a.grad_scale, (long)a.n, s, a.dyn);
   return hipGetLastError();
 }
 

@@ -519,7 +519,7 @@ Tensor sumsq(const Tensor& x) {
 
 void adamw_flat(Tensor param, const Tensor& grad, Tensor exp_avg, Tensor exp_avg_sq, const c10::optional<Tensor>& shadow,
                 double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
-                const c10::optional<Tensor>& grad_scale) {
+                const c10::optional<Tensor>& grad_scale, const c10::optional<Tensor>& dyn) {
   for (const Tensor* t : {static_cast<const Tensor*>(&param), &grad, static_cast<const Tensor*>(&exp_avg),
                           static_cast<const Tensor*>(&exp_avg_sq)}) {
     check_gpu(*t, "adamw buffer");
@@ -552,7 +552,30 @@ void adamw_flat(Tensor param, const Tensor& grad, Tensor exp_avg, Tensor exp_avg
   a.weight_decay = (float)weight_decay;
   a.bias_correction1 = (float)(1.0 - std::pow(beta1, (double)step));
   a.bias_correction2_sqrt = (float)std::sqrt(1.0 - std::pow(beta2, (double)step));
+  if (dyn.has_value()) {
+    check_gpu(*dyn, "adamw dyn scalars");
+    check_dtype(*dyn, at::kFloat, "adamw dyn scalars");
+    TORCH_CHECK(dyn->numel() == 3 && dyn->is_contiguous(), "adamw dyn scalars: 3 contiguous floats");
+    a.dyn = dyn->data_ptr<float>();
+  }
   check_hip(llmt::launch_adamw_flat(a, cur_stream()), "adamw_flat");
+}
+
+// {decay, step_size, bc2_sqrt} of one AdamW step exactly as adamw_flat forms them (CPU tensor): the
+// host stages them into adamw_flat's `dyn` before each hipGraph replay of a captured step
+Tensor adamw_stage_scalars(double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step) {
+  TORCH_CHECK(step >= 1, "adamw step must be >= 1");
+  llmt::AdamWArgs a{};
+  a.lr = (float)lr;
+  a.beta1 = (float)beta1;
+  a.beta2 = (float)beta2;
+  a.eps = (float)eps;
+  a.weight_decay = (float)weight_decay;
+  a.bias_correction1 = (float)(1.0 - std::pow(beta1, (double)step));
+  a.bias_correction2_sqrt = (float)std::sqrt(1.0 - std::pow(beta2, (double)step));
+  Tensor out = at::empty({3}, at::TensorOptions().dtype(at::kFloat));
+  llmt::adamw_step_scalars(a, out.data_ptr<float>());
+  return out;
 }
 
 }  // namespace
@@ -583,7 +606,10 @@ TORCH_LIBRARY(llmtrain_hip, m) {
         " Tensor(a!)? dbias=None, int seq_len=0) -> (Tensor, Tensor?)");
   m.def("sumsq(Tensor x) -> Tensor");
   m.def("adamw_flat(Tensor(a!) param, Tensor grad, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor(d!)? shadow,"
-        " float lr, float beta1, float beta2, float eps, float weight_decay, int step, Tensor? grad_scale) -> ()");
+        " float lr, float beta1, float beta2, float eps, float weight_decay, int step, Tensor? grad_scale,"
+        " Tensor? dyn=None) -> ()");
+  m.def("adamw_stage_scalars(float lr, float beta1, float beta2, float eps, float weight_decay, int step) -> Tensor",
+        &adamw_stage_scalars);
 }
 
 TORCH_LIBRARY_IMPL(llmtrain_hip, CUDA, m) {

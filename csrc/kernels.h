@@ -123,8 +123,13 @@ struct AdamWArgs {
   long long n;
   float lr, beta1, beta2, eps, weight_decay;
   float bias_correction1, bias_correction2_sqrt;
+  // optional device [decay, step_size, bc2_sqrt]: per-step scalars staged by the host before a
+  // hipGraph replay of the training step (the by-value ones above would be baked into the graph)
+  const float* dyn;
 };
 hipError_t launch_adamw_flat(const AdamWArgs& a, hipStream_t stream);
+// the three per-step scalars exactly as launch_adamw_flat forms them: {decay, step_size, bc2_sqrt}
+void adamw_step_scalars(const AdamWArgs& a, float out[3]);
 // out (device scalar) = sum(x^2); `partials` must hold kSumsqBlocks floats
 constexpr int kSumsqBlocks = 1024;
 hipError_t launch_sumsq(const float* x, long long n, float* partials, float* out,

@@ -293,12 +293,18 @@ def sumsq(x):
     return ref.sumsq(x)
 
 
-def adamw_flat(param, grad, exp_avg, exp_avg_sq, shadow, *, lr, beta1, beta2, eps, weight_decay, step, grad_scale):
+def adamw_flat(
+    param, grad, exp_avg, exp_avg_sq, shadow, *, lr, beta1, beta2, eps, weight_decay, step, grad_scale, dyn=None
+):
+    """``dyn`` (GPU only): device ``[decay, step_size, bc2_sqrt]`` read by the kernel instead of the
+    values formed from ``lr``/``step`` — a hipGraph-captured step stages them before each replay."""
     if _on_gpu(param):
         hip_ops().adamw_flat(
-            param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps, weight_decay, step, grad_scale
+            param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps, weight_decay, step, grad_scale, dyn
         )
         return
+    if dyn is not None:
+        raise ValueError("adamw_flat: device-staged scalars exist only on the GPU path")
     ref.adamw_flat(
         param, grad, exp_avg, exp_avg_sq, shadow, lr=lr, beta1=beta1, beta2=beta2, eps=eps,
         weight_decay=weight_decay, step=step, grad_scale=grad_scale,

@@ -61,6 +61,7 @@ class FusedAdamW(torch.optim.Optimizer):
         self.exp_avg_sq = torch.zeros_like(store.master)
         self._step_count_host = 0
         self._step_tensor = torch.zeros((), dtype=torch.float32)
+        self._dyn: torch.Tensor | None = None  # device per-step scalars of a graph-captured step
 
     # -- torch-compatible state -----------------------------------------------------------
 
@@ -142,6 +143,42 @@ class FusedAdamW(torch.optim.Optimizer):
         )
         self.store.mark_shadow_synced()
         return loss
+
+
+    # -- hipGraph-captured steps (Trainer with trainer.extra.cuda_graph) --------------------
+
+    def stage_graph_step(self) -> None:
+        """Host half of a graph-replayed step: advance the step counter and stage this step's
+        ``{decay, step_size, bc2_sqrt}`` (from the CURRENT lr, i.e. after the scheduler) into the
+        device buffer the captured AdamW kernel reads — the same values :meth:`step` would bake in."""
+        self._materialize_state()
+        group = self.param_groups[0]
+        beta1, beta2 = group["betas"]
+        self._step_count_host += 1
+        self._step_tensor.fill_(float(self._step_count_host))
+        host = torch.ops.llmtrain_hip.adamw_stage_scalars(
+            float(group["lr"]), float(beta1), float(beta2), float(group["eps"]), float(group["weight_decay"]),
+            self._step_count_host,
+        )
+        if self._dyn is None:
+            self._dyn = torch.empty(3, dtype=torch.float32, device=self.store.master.device)
+        self._dyn.copy_(host)
+
+    @torch.no_grad()
+    def step_captured(self, *, grad_scale: torch.Tensor | None = None) -> None:
+        """Device half, recorded into the graph: the AdamW kernel reading the staged scalars (no host
+        state changes, so a capture followed by replays counts each replay exactly once)."""
+        if self._dyn is None:
+            raise RuntimeError("stage_graph_step() must run before the captured step")
+        group = self.param_groups[0]
+        beta1, beta2 = group["betas"]
+        ops.adamw_flat(
+            self.store.master, self.store.grad, self.exp_avg, self.exp_avg_sq, self.store.shadow,
+            lr=float(group["lr"]), beta1=float(beta1), beta2=float(beta2), eps=float(group["eps"]),
+            weight_decay=float(group["weight_decay"]), step=max(1, self._step_count_host), grad_scale=grad_scale,
+            dyn=self._dyn,
+        )
+        self.store.mark_shadow_synced()
 
 
 def fused_clip_coef(store: Any, max_norm: float) -> tuple[torch.Tensor, torch.Tensor]:

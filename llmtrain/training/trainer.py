@@ -21,6 +21,9 @@ What changes on the MI355X path:
   that rank raises at that step of a run that did not resume — one simulated crash per job),
   ``profile`` (torch.profiler window), ``bucket_cap_mb``, ``grad_reduce_dtype``,
   ``async_checkpoint`` (GPU default true: pinned snapshot + background write);
+* ``trainer.extra.cuda_graph`` (single GPU, fused engine, dropout 0): after ``cuda_graph_warmup``
+  eager steps the whole optimizer step is captured once as a hipGraph and replayed
+  (:mod:`llmtrain.training.graph_step`) — for the launch-bound small presets;
 * ``train/allreduce_ms`` (max over ranks) logs the exposed gradient all-reduce time of the flat
   reducer — the part of the communication NOT hidden behind the backward.
 """
@@ -50,6 +53,7 @@ from llmtrain.runtime.device import decorrelate_rank_streams, resolve_policy, se
 from llmtrain.runtime.tuning import enable_tuned_gemms
 from llmtrain.tracking import NullTracker, Tracker
 from llmtrain.training.checkpoint import CheckpointManager, CheckpointPayload, restore_rng_states
+from llmtrain.training.graph_step import GraphedStep, check_graphable
 from llmtrain.training.optim import FusedAdamW, build_optimizer, fused_clip_coef
 
 __all__ = ["TrainResult", "Trainer", "lr_lambda_factory"]
@@ -203,6 +207,16 @@ class Trainer:
             self._ckpt_mgr = CheckpointManager(run_dir / "checkpoints", keep_last_k=keep, async_write=async_ckpt)
         self._run_dir = run_dir
         self.last_grad_norm: torch.Tensor | None = None
+        self._graphed: GraphedStep | None = None
+        if bool(cfg.trainer.extra.get("cuda_graph", False)):
+            check_graphable(
+                device=self._device, fused=self._policy.use_fused, optimizer=self._optimizer,
+                ddp_active=self._is_ddp_active, dropout=float(cfg.model.dropout),
+            )
+            self._graphed = GraphedStep(
+                device=self._device, optimizer=self._optimizer, eager=self._eager_step, body=self._captured_step,
+                after=self._scheduler.step, warmup=int(cfg.trainer.extra.get("cuda_graph_warmup", 2)),
+            )
         logger.info(
             "trainer: device=%s compute_dtype=%s fused=%s ddp=%s",
             self._device, self._policy.compute_dtype, self._policy.use_fused, self._is_ddp_active,
@@ -375,19 +389,49 @@ class Trainer:
         ``bench.py`` times exactly this method.
         """
         accum = self._cfg.trainer.grad_accum_steps
-        self._optimizer.zero_grad()
-        step_loss = torch.zeros((), dtype=torch.float32, device=self._device)
+        if self._graphed is not None:  # trainer.extra.cuda_graph: replay the captured step
+            host = [_drop_dense_mask(batches.next()) for _ in range(accum)]
+            tokens = sum(int(b["input_ids"].numel()) for b in host)
+            loss, self.last_grad_norm = self._graphed.step(host)
+            return loss, tokens
+        dev_batches = []
         tokens = 0
-        for micro in range(accum):
+        for _ in range(accum):
             batch = _to_device(batches.next(), self._device)
             tokens += batch["input_ids"].numel()
+            dev_batches.append(batch)
+        loss, _ = self._eager_step(dev_batches)
+        return loss, tokens
+
+    def _eager_step(self, dev_batches: list[dict[str, Any]]) -> tuple[torch.Tensor, torch.Tensor]:
+        """Micro-batch forward/backward (communication on the last only), clip, AdamW, LR step."""
+        accum = len(dev_batches)
+        self._optimizer.zero_grad()
+        step_loss = torch.zeros((), dtype=torch.float32, device=self._device)
+        for micro, batch in enumerate(dev_batches):
             with self._sync_context(micro == accum - 1):
                 with self._policy.autocast():
                     loss, metrics = self._adapter.compute_loss(self._model, batch)
                 (loss / accum).backward()
             step_loss += _loss_tensor(loss, metrics)
         self._optimizer_step()
-        return step_loss / accum, tokens
+        assert self.last_grad_norm is not None
+        return step_loss / accum, self.last_grad_norm
+
+    def _captured_step(self, static: list[dict[str, Any]]) -> tuple[torch.Tensor, torch.Tensor]:
+        """The body recorded into the hipGraph (single process, fused engine + fused AdamW): no
+        host-side optimizer state changes here — :class:`GraphedStep` stages them per replay."""
+        accum = len(static)
+        self._optimizer.zero_grad()
+        step_loss = torch.zeros((), dtype=torch.float32, device=self._device)
+        for batch in static:
+            with self._policy.autocast():
+                loss, metrics = self._adapter.compute_loss(self._model, batch)
+            (loss / accum).backward()
+            step_loss += _loss_tensor(loss, metrics)
+        norm, coef = fused_clip_coef(self._optimizer.store, self._cfg.trainer.max_grad_norm)
+        self._optimizer.step_captured(grad_scale=coef)
+        return step_loss / accum, norm
 
     def _fault_rank(self) -> bool:
         """``trainer.extra.fail_rank`` (default: every rank) picks the rank that crashes."""

@@ -152,3 +152,28 @@ def test_gpu_shape_fallback_is_opt_in() -> None:
     assert settle_fused_path(gpu, cfg({}), supported=True).use_fused
     cpu = RuntimePolicy(device=torch.device("cpu"), compute_dtype=torch.float32, use_fused=True)
     assert not settle_fused_path(cpu, cfg({}), supported=False).use_fused
+
+
+def test_cuda_graph_requirements_are_checked() -> None:
+    """trainer.extra.cuda_graph (llmtrain.training.graph_step): every unmet requirement of a
+    captured step is a config error naming it, not a silent eager run."""
+    import torch
+
+    from llmtrain.training.graph_step import check_graphable
+    from llmtrain.training.optim import FusedAdamW
+
+    class _FakeFused(FusedAdamW):  # isinstance check only
+        def __init__(self) -> None:  # noqa: D107 - no store needed
+            pass
+
+    ok = dict(device=torch.device("cuda"), fused=True, optimizer=_FakeFused(), ddp_active=False, dropout=0.0)
+    check_graphable(**ok)
+    for key, bad, word in [
+        ("device", torch.device("cpu"), "GPU"),
+        ("fused", False, "fused engine"),
+        ("optimizer", object(), "fused AdamW"),
+        ("ddp_active", True, "single-process"),
+        ("dropout", 0.1, "dropout"),
+    ]:
+        with pytest.raises(ValueError, match=word):
+            check_graphable(**{**ok, key: bad})

@@ -222,6 +222,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
                                                           float* __restrict__ dq_part, float* __restrict__ vparts,
                                                           int T, int H, int nkb, DropoutArgs dr, int hd_arg,
                                                           float scale_arg, const uint8_t* __restrict__ key_valid) {
+  resolve_dropout(dr);
   __shared__ __attribute__((aligned(16))) bf16_raw kt_lds[kHD * kKvBlk];             // K^T, 32 KB
   __shared__ __attribute__((aligned(16))) bf16_raw qd_lds[2][2][kQTile * kHD];      // [buf][Q|dO] 32 KB
   __shared__ __attribute__((aligned(16))) bf16_raw ds_lds[2][kKvBlk * kQTile];      // [buf][key][q] 64 KB
@@ -611,6 +612,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd128_kernel(const bf16_raw* __r
                                                              float* __restrict__ dq_part, float* __restrict__ vparts,
                                                              int T, int H, int nkb, DropoutArgs dr,
                                                              const uint8_t* __restrict__ key_valid) {
+  resolve_dropout(dr);
   constexpr int hd = 2 * kHD;
   __shared__ __attribute__((aligned(16))) bf16_raw qd_lds[2][2][2][kQTile * kHD];  // [buf][Q|dO][half] 64 KB
   __shared__ __attribute__((aligned(16))) bf16_raw ds_lds[2][kKv128 * kQTile];     // [buf][key][q] 32 KB

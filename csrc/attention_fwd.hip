@@ -76,6 +76,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
                                                           float* __restrict__ lse, int T, int H,
                                                           int nqb, DropoutArgs dr, int hd_arg, float c_arg,
                                                           const uint64_t* __restrict__ key_bits) {
+  resolve_dropout(dr);
   __shared__ __attribute__((aligned(16))) bf16_raw smem[2][2][NH][kKBlk * kHD];  // [buf][K|V][half][tile]
   const int lane = threadIdx.x & 63;
   // readfirstlane makes the wave index (and every tile/mask decision derived from it) provably

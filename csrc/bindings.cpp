@@ -46,11 +46,16 @@ bool is_lowp(const Tensor& t, const char* name) {
 
 // dropout probability + site seed -> kernel arguments (thr = round(p * 2^16); the scale uses the
 // quantised keep probability so the mask stays unbiased)
+// set_dropout_seed_offset: a device word every dropout kernel launched while it is set adds to its
+// site seed (hipGraph-captured steps: the word is restaged per replay; nullptr = off)
+const uint32_t* g_seed_add = nullptr;
+
 llmt::DropoutArgs make_dropout(double p, int64_t seed) {
   TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout p must be in [0, 1)");
   llmt::DropoutArgs d{};
   const uint32_t thr = (uint32_t)std::lround(p * 65536.0);
   if (thr == 0) return d;
+  d.seed_add = g_seed_add;
   d.seed = (uint32_t)(seed & 0xffffffffLL);
   d.thr = thr > 65535u ? 65535u : thr;
   d.scale = 65536.0f / (float)(65536u - d.thr);
@@ -399,6 +404,15 @@ Tensor attn_bwd(const Tensor& dout, const Tensor& qkv, const Tensor& out, const 
 
 // process-wide deterministic mode (run.deterministic): fixed-order split-K / embedding reductions
 void set_deterministic(bool on) { llmt::set_deterministic(on); }
+void set_dropout_seed_offset(const c10::optional<Tensor>& word) {
+  if (!word.has_value()) {
+    g_seed_add = nullptr;
+    return;
+  }
+  check_gpu(*word, "dropout seed offset");
+  TORCH_CHECK(word->scalar_type() == at::kInt && word->numel() >= 1, "dropout seed offset: int32 device word");
+  g_seed_add = reinterpret_cast<const uint32_t*>(word->data_ptr<int32_t>());
+}
 bool get_deterministic() { return llmt::deterministic(); }
 
 // keep-mask of `n` consecutive elements of one dropout site (tests / debugging)
@@ -601,6 +615,7 @@ TORCH_LIBRARY(llmtrain_hip, m) {
   m.def("dropout_mask(int n, float p, int seed, Tensor like) -> Tensor");
   m.def("set_deterministic(bool on) -> ()", &set_deterministic);  // catch-all: no tensor arguments
   m.def("get_deterministic() -> bool", &get_deterministic);
+  m.def("set_dropout_seed_offset(Tensor? word) -> ()", &set_dropout_seed_offset);
   m.def("wgrad_gemm(Tensor dy, Tensor x, Tensor(a!) c, int split=0, int tile=0, int pipe=-1) -> ()");
   m.def("gemm_fused(Tensor a, Tensor b, bool b_kn, int epilogue, Tensor? bias=None, Tensor? u=None,"
         " Tensor(a!)? dbias=None, int seq_len=0) -> (Tensor, Tensor?)");

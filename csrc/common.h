@@ -71,6 +71,11 @@ __device__ __forceinline__ uint32_t drop_hash(uint32_t seed, uint64_t pair) {
   return mix32((uint32_t)pair ^ seed ^ (uint32_t)(pair >> 32) * 0x85ebca6bu);
 }
 
+// per-step seed offset of a graph-replayed step (DropoutArgs::seed_add), applied once at kernel entry
+__device__ __forceinline__ void resolve_dropout(DropoutArgs& d) {
+  if (d.seed_add != nullptr) d.seed += *d.seed_add;
+}
+
 __device__ __forceinline__ bool drop_keep(uint32_t seed, uint32_t thr, uint64_t e) {
   const uint32_t h = drop_hash(seed, e >> 1);
   return ((e & 1) ? (h >> 16) : (h & 0xffffu)) >= thr;

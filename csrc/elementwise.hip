@@ -156,6 +156,7 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __res
                                                             const float* __restrict__ wpe,
                                                             float* __restrict__ x, int M, int T,
                                                             int d, int V, DropoutArgs dr) {
+  resolve_dropout(dr);
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
   const int lane = threadIdx.x & 63;
@@ -183,6 +184,7 @@ __global__ __launch_bounds__(256) void embedding_bwd_tok_kernel(const float* __r
                                                                 const int64_t* __restrict__ ids,
                                                                 float* __restrict__ dwte, int M,
                                                                 int d, int V, DropoutArgs dr) {
+  resolve_dropout(dr);
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
   const int lane = threadIdx.x & 63;
@@ -202,6 +204,7 @@ __global__ __launch_bounds__(256) void embedding_bwd_tok_kernel(const float* __r
 __global__ __launch_bounds__(256) void embedding_bwd_pos_kernel(const float* __restrict__ dx,
                                                                 float* __restrict__ dwpe, int B,
                                                                 int T, int d, DropoutArgs dr) {
+  resolve_dropout(dr);
   const int d4 = d >> 2;
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long)T * d4) return;
@@ -221,6 +224,7 @@ __global__ __launch_bounds__(256) void embedding_bwd_pos_kernel(const float* __r
 }
 
 __global__ __launch_bounds__(256) void dropout_mask_kernel(DropoutArgs dr, bool* __restrict__ out, long long n) {
+  resolve_dropout(dr);
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = dr.thr == 0 || drop_keep(dr.seed, dr.thr, (uint64_t)i);
 }

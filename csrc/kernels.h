@@ -18,6 +18,9 @@ struct DropoutArgs {
   uint32_t seed = 0;
   uint32_t thr = 0;
   float scale = 1.f;
+  // optional device word added to `seed` at kernel entry: a hipGraph-captured step keeps its
+  // captured site seeds and gets fresh masks per replay from the host-staged offset
+  const uint32_t* seed_add = nullptr;
 };
 
 struct LnFwdArgs {

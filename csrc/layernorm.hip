@@ -52,6 +52,7 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
     const float* __restrict__ x, const TD* __restrict__ delta, const float* __restrict__ w,
     const float* __restrict__ b, float* __restrict__ xs_out, TY* __restrict__ y,
     float* __restrict__ mean_out, float* __restrict__ rstd_out, int M, int d, float eps, DropoutArgs dr) {
+  resolve_dropout(dr);
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * kLnWaves + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -156,6 +157,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const float* __restrict__ rstd, const float* __restrict__ w, const float* __restrict__ dresid,
     const float* __restrict__ dy_scale, float* __restrict__ dx, TDY* __restrict__ dx_lp,
     float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dproj, int M, int d, DropoutArgs dr) {
+  resolve_dropout(dr);
   extern __shared__ __attribute__((aligned(16))) float smem[];  // [kBwdWaves][d], reused per accumulator
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nc = d >> 2;
@@ -315,6 +317,7 @@ __global__ __launch_bounds__(256, ROWS == 1 ? (MAXC <= 3 ? 4 : 2) : 3) void ln_b
     const float* __restrict__ rstd, const float* __restrict__ w, const float* __restrict__ dresid,
     const float* __restrict__ dy_scale, float* __restrict__ dx, TDY* __restrict__ dx_lp,
     float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dproj, int M, int d, DropoutArgs dr) {
+  resolve_dropout(dr);
   extern __shared__ __attribute__((aligned(16))) float smem[];  // [kBwdWaves][d]
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nc = d >> 2;

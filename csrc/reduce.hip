@@ -85,6 +85,7 @@ __global__ __launch_bounds__(256) void embedding_bwd_sorted_kernel(const float* 
                                                                    const int64_t* __restrict__ order,
                                                                    float* __restrict__ dwte, int M, int d, int V,
                                                                    DropoutArgs dr) {
+  resolve_dropout(dr);
   const long i = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= M) return;
   const int64_t tok = sorted_ids[i];

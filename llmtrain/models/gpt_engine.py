@@ -190,6 +190,8 @@ class FusedGPTEngine:
         self.segment_order = [name for name, _ in groups]
         self.store = FlatParamStore(groups, shadow_dtype=compute_dtype, pad_last_rows=VOCAB_PAD)
         self.grad_ready: Callable[[str], None] | None = None
+        # per-forward dropout base seed provider (None: one draw from torch's CPU generator)
+        self.drop_seed_source: Callable[[], int] | None = None
         self._anchor = torch.zeros((), requires_grad=True, device=self.store.device)
         self.wgrad_impl = os.environ.get("LLMTRAIN_WGRAD", "hip")
         # weight-gradient GEMMs on a second HIP stream, overlapping the dX GEMMs and the
@@ -345,7 +347,10 @@ class FusedGPTEngine:
         if m.training and m.dropout > 0.0:
             # one host draw per forward from torch's (seeded, checkpointed) CPU generator
             state.drop_p = float(m.dropout)
-            state.drop_seed = int(torch.randint(0, 2**31 - 1, (1,)).item())
+            if self.drop_seed_source is not None:  # a hipGraph-captured step (training/graph_step.py)
+                state.drop_seed = int(self.drop_seed_source())
+            else:
+                state.drop_seed = int(torch.randint(0, 2**31 - 1, (1,)).item())
 
         if mask is not None:
             # key padding (no host sync: a mask is taken as given; the trainer drops all-ones masks

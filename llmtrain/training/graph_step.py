@@ -10,11 +10,16 @@ and replays it for every later step; the host then only copies the next batch in
 static input buffers, stages the step's AdamW scalars (:meth:`FusedAdamW.stage_graph_step`: the
 learning rate changes every step and must not be baked in) and launches the graph.
 
+Dropout: the captured kernels keep their site seeds; every dropout kernel also adds a device
+word to its seed at entry (``set_dropout_seed_offset``), which the host restages before each
+step.  In this mode the per-forward base seed is the micro-batch index and the word is a hash of
+(run seed, optimizer step), for eager and replayed steps alike — fresh masks every step, and a
+resumed run replays the same masks (no dependence on how many RNG draws happened before).
+
 Scope (checked when the trainer is built, :func:`check_graphable`): the fused engine on a GPU,
-the fused AdamW, one process (RCCL collectives are not captured), dropout 0 (per-step dropout
-seeds are host values), and batches of one fixed shape without padding.  A batch that does not
-fit the captured shape or carries a padding mask runs eagerly instead (same results, just
-launch-bound), so correctness never depends on the data.  The first ``warmup`` steps run
+the fused AdamW, one process (RCCL collectives are not captured), and batches of one fixed
+shape without padding.  A batch that does not fit the captured shape or carries a padding mask
+runs eagerly instead (same results, just launch-bound), so correctness never depends on the data.  The first ``warmup`` steps run
 eagerly on the capture stream (library handles, workspaces and caches are created outside the
 capture), then the step is captured and replayed.
 """
@@ -32,7 +37,7 @@ __all__ = ["GraphedStep", "check_graphable"]
 logger = logging.getLogger(__name__)
 
 
-def check_graphable(*, device: torch.device, fused: bool, optimizer: Any, ddp_active: bool, dropout: float) -> None:
+def check_graphable(*, device: torch.device, fused: bool, optimizer: Any, ddp_active: bool) -> None:
     """Raise ``ValueError`` naming the first requirement of a captured step that is not met."""
     from llmtrain.training.optim import FusedAdamW
 
@@ -44,8 +49,6 @@ def check_graphable(*, device: torch.device, fused: bool, optimizer: Any, ddp_ac
         raise ValueError("trainer.extra.cuda_graph needs the fused AdamW")
     if ddp_active:
         raise ValueError("trainer.extra.cuda_graph is single-process (RCCL collectives are not captured)")
-    if dropout > 0.0:
-        raise ValueError("trainer.extra.cuda_graph needs model.dropout 0 (dropout seeds are per-step host values)")
 
 
 class GraphedStep:
@@ -65,6 +68,9 @@ class GraphedStep:
         body: Callable[[list[dict[str, Any]]], tuple[torch.Tensor, torch.Tensor]],
         after: Callable[[], None],
         warmup: int = 2,
+        engine: Any = None,
+        dropout: bool = False,
+        run_seed: int = 0,
     ) -> None:
         self._device = device
         self._opt = optimizer
@@ -79,6 +85,37 @@ class GraphedStep:
         self._out: tuple[torch.Tensor, torch.Tensor] | None = None
         self.replays = 0
         self.eager_steps = 0
+        self._run_seed = int(run_seed) & 0xFFFFFFFF
+        self._seed_word: torch.Tensor | None = None
+        self._micro = 0
+        if dropout:
+            if engine is None:
+                raise ValueError("graph-captured dropout needs the fused engine")
+            self._seed_word = torch.zeros(1, dtype=torch.int32, device=device)
+            engine.drop_seed_source = self._next_base
+
+    # -- dropout seeds -----------------------------------------------------------------------
+
+    def _next_base(self) -> int:
+        """Base seed of the next forward in this step: its micro-batch index (captured once)."""
+        base = 0x5EED0000 + self._micro
+        self._micro += 1
+        return base
+
+    def _stage_dropout(self, step_no: int) -> None:
+        if self._seed_word is None:
+            return
+        from llmtrain.ops.reference import mix32_int
+
+        word = mix32_int(self._run_seed ^ ((step_no * 0x9E3779B9) & 0xFFFFFFFF))
+        word = word - (1 << 32) if word >= (1 << 31) else word  # int32 view of the uint32
+        self._micro = 0
+        self._seed_word.fill_(word)
+
+    def _kernels_read_word(self, on: bool) -> None:
+        """Dropout kernels launched (or captured) while on add the staged word to their seeds."""
+        if self._seed_word is not None:
+            torch.ops.llmtrain_hip.set_dropout_seed_offset(self._seed_word if on else None)
 
     # -- input handling --------------------------------------------------------------------
 
@@ -110,13 +147,22 @@ class GraphedStep:
         """One optimizer step over ``host_batches`` (the micro-batches, CPU tensors, padding masks
         already dropped where all-ones); returns ``(mean loss, pre-clip grad norm)`` as device
         scalars that later steps do not overwrite."""
+        self._stage_dropout(self._opt._step_count_host + 1)
         if self._calls < self._warmup or not self._graphable(host_batches):
             self._calls += 1
             self.eager_steps += 1
-            return self._eager_on_stream(host_batches)
+            self._kernels_read_word(True)
+            try:
+                return self._eager_on_stream(host_batches)
+            finally:
+                self._kernels_read_word(False)
         self._calls += 1
         if self._graph is None:
-            self._capture(host_batches)
+            self._kernels_read_word(True)
+            try:
+                self._capture(host_batches)
+            finally:
+                self._kernels_read_word(False)
         else:
             self._to_static(host_batches)
             self._opt.stage_graph_step()

@@ -21,7 +21,7 @@ What changes on the MI355X path:
   that rank raises at that step of a run that did not resume — one simulated crash per job),
   ``profile`` (torch.profiler window), ``bucket_cap_mb``, ``grad_reduce_dtype``,
   ``async_checkpoint`` (GPU default true: pinned snapshot + background write);
-* ``trainer.extra.cuda_graph`` (single GPU, fused engine, dropout 0): after ``cuda_graph_warmup``
+* ``trainer.extra.cuda_graph`` (single GPU, fused engine): after ``cuda_graph_warmup``
   eager steps the whole optimizer step is captured once as a hipGraph and replayed
   (:mod:`llmtrain.training.graph_step`) — for the launch-bound small presets;
 * ``train/allreduce_ms`` (max over ranks) logs the exposed gradient all-reduce time of the flat
@@ -211,11 +211,13 @@ class Trainer:
         if bool(cfg.trainer.extra.get("cuda_graph", False)):
             check_graphable(
                 device=self._device, fused=self._policy.use_fused, optimizer=self._optimizer,
-                ddp_active=self._is_ddp_active, dropout=float(cfg.model.dropout),
+                ddp_active=self._is_ddp_active,
             )
             self._graphed = GraphedStep(
                 device=self._device, optimizer=self._optimizer, eager=self._eager_step, body=self._captured_step,
                 after=self._scheduler.step, warmup=int(cfg.trainer.extra.get("cuda_graph_warmup", 2)),
+                engine=getattr(unwrap(self._model), "engine", None), dropout=float(cfg.model.dropout) > 0.0,
+                run_seed=int(cfg.run.seed),
             )
         logger.info(
             "trainer: device=%s compute_dtype=%s fused=%s ddp=%s",

@@ -166,14 +166,13 @@ def test_cuda_graph_requirements_are_checked() -> None:
         def __init__(self) -> None:  # noqa: D107 - no store needed
             pass
 
-    ok = dict(device=torch.device("cuda"), fused=True, optimizer=_FakeFused(), ddp_active=False, dropout=0.0)
+    ok = dict(device=torch.device("cuda"), fused=True, optimizer=_FakeFused(), ddp_active=False)
     check_graphable(**ok)
     for key, bad, word in [
         ("device", torch.device("cpu"), "GPU"),
         ("fused", False, "fused engine"),
         ("optimizer", object(), "fused AdamW"),
         ("ddp_active", True, "single-process"),
-        ("dropout", 0.1, "dropout"),
     ]:
         with pytest.raises(ValueError, match=word):
             check_graphable(**{**ok, key: bad})

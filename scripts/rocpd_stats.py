@@ -21,7 +21,7 @@ def main() -> None:
     top = int(sys.argv[3]) if len(sys.argv) > 3 else 30
     con = sqlite3.connect(db)
     rows = con.execute("select name, stream_id, start, end from kernels order by start").fetchall()
-    marks = [r[3] for r in rows if "adamw_kernel" in r[0]]
+    marks = [r[3] for r in rows if "adamw_kernel" in r[0] or "adamw_tiled_kernel" in r[0]]
     if len(marks) <= skip + 1:
         raise SystemExit(f"only {len(marks)} optimizer steps in the trace")
     t0, t1 = marks[skip], marks[-1]

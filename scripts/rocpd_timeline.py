@@ -20,7 +20,7 @@ def main() -> None:
     idx = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     con = sqlite3.connect(db)
     rows = con.execute("select name, stream_id, start, end from kernels order by start").fetchall()
-    marks = [r[3] for r in rows if "adamw_kernel" in r[0]]
+    marks = [r[3] for r in rows if "adamw_kernel" in r[0] or "adamw_tiled_kernel" in r[0]]
     t0, t1 = marks[idx], marks[idx + 1]
     step = [r for r in rows if r[2] >= t0 and r[3] <= t1]
     ce_end = next((e for n, _, _, e in step if "ce_fwd_bwd" in n), t0)

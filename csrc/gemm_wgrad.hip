@@ -316,9 +316,11 @@ Plan plan_for(int tile, int M, int N, int K, int split_req, int ncu, int min_spl
   p.tiles_k = (K + bk - 1) / bk;
   p.tiles = tiles_n * p.tiles_k;
   const int slots = ncu * (tile == 256 ? 1 : 2);
-  // per resident workgroup; chip rates measured at M = 65536 (bench/micro.py wgrad):
-  // <4,4> 0.9-1.0 PF on 768..3072-wide outputs, <2,2> 0.76-0.87 PF
-  const double rate_cu = (tile == 256 ? 1.0e15 : 0.85e15) / ncu * (tile == 256 ? 1.0 : 0.5);
+  // per resident workgroup; chip rates measured at M = 65536 (bench/micro.py wgrad): <4,4> 0.9-1.0 PF
+  // on 768..3072-wide outputs, <2,2> 0.76-0.87 PF solo — but inside the step (side stream, sharing
+  // the chip) the 128 tile's half arithmetic intensity costs more: modelled at 0.6 PF, GPT-2 XL
+  // forced to 256 tiles measured +2.7 % (profiles/r2/ab_xl_wgrad_tile.txt) where 0.85 picked 128
+  const double rate_cu = (tile == 256 ? 1.0e15 : 0.6e15) / ncu * (tile == 256 ? 1.0 : 0.5);
   const int max_split = (M + BM - 1) / BM;
   auto eval = [&](int s, Plan& out) {
     int chunk = (M + s - 1) / s;

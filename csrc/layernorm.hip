@@ -429,6 +429,136 @@ __global__ __launch_bounds__(256, ROWS == 1 ? (MAXC <= 3 ? 4 : 2) : 3) void ln_b
   }
 }
 
+// Split-row backward for wide rows (GPT-2 XL's d = 1600): a workgroup's 4 waves take 2 rows per
+// iteration, each row split into two column halves held by two waves, so a wave keeps half a row
+// (MAXC = 7 -> 4 float4 chunks per lane) and the kernel stays at <= 168 VGPRs — one wave then fits
+// on a SIMD beside the side stream's weight-gradient GEMM (336 of 512 registers), where the
+// whole-row kernel's 256 did not.  The two halves' row sums meet in LDS (one barrier per row
+// pair, parity double-buffered); column partials and the per-wave dproj rows are summed over the
+// two row slots at the end (fixed order).
+template <int MAXC, typename TDY, bool LOWP_OUT>
+__global__ __launch_bounds__(256, 3) void ln_bwd_split_kernel(
+    const TDY* __restrict__ dy, const float* __restrict__ xs, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const float* __restrict__ w, const float* __restrict__ dresid,
+    const float* __restrict__ dy_scale, float* __restrict__ dx, TDY* __restrict__ dx_lp,
+    float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dproj, int M, int d, DropoutArgs dr) {
+  resolve_dropout(dr);
+  constexpr int HC = (MAXC + 1) / 2;  // float4 chunks per lane for half a row
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // [4][d]: 0-1 staging, 2-3 dproj
+  __shared__ float red[2][2][2][2];                              // [parity][slot][half][s1|s2]
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int slot = wid >> 1, half = wid & 1;
+  const int nc = d >> 2, nh0 = (nc + 1) >> 1;
+  const int cbase = half ? nh0 : 0, nhalf = half ? nc - nh0 : nh0;
+  const float scale = dy_scale != nullptr ? *dy_scale : 1.f;
+  const float inv_d = 1.f / (float)d;
+  const bool has_pp = dproj != nullptr;
+  const float4_t zero = {0.f, 0.f, 0.f, 0.f};
+  float* pp = smem + (2 + slot) * d;  // this row slot's dproj partial (this wave's half of it)
+
+  float4_t pw[HC], pb[HC];
+#pragma unroll
+  for (int j = 0; j < HC; ++j) {
+    pw[j] = zero; pb[j] = zero;
+    const int cl = lane + j * 64;
+    if (has_pp && cl < nhalf) store4(pp + 4 * (cbase + cl), zero);
+  }
+
+  int par = 0;
+  for (long pr = blockIdx.x; 2 * pr < M; pr += gridDim.x, par ^= 1) {  // uniform over the workgroup
+    const long row0 = 2 * pr + slot;
+    const bool live = row0 < M;  // wave-uniform
+    const long row = live ? row0 : 0;
+    const float mu = mean[row], rs = rstd[row];
+    const float* wr = w + __builtin_amdgcn_readfirstlane((int)(row >> 40));
+    float4_t g[HC], xh[HC], rr[HC];
+#pragma unroll
+    for (int j = 0; j < HC; ++j) {
+      const int cl = lane + j * 64, c = cbase + (cl < nhalf ? cl : 0);
+      g[j] = load4(dy + row * d + 4 * c);
+      xh[j] = load4_nt(xs + row * d + 4 * c);
+    }
+    if (dresid != nullptr) {
+#pragma unroll
+      for (int j = 0; j < HC; ++j) {
+        const int cl = lane + j * 64, c = cbase + (cl < nhalf ? cl : 0);
+        rr[j] = load4_nt(dresid + row * d + 4 * c);
+      }
+    }
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < HC; ++j) {
+      const int cl = lane + j * 64, c = cbase + (cl < nhalf ? cl : 0);
+      const bool ok = live && cl < nhalf;
+      g[j] = ok ? g[j] * scale : zero;
+      xh[j] = ok ? (xh[j] - mu) * rs : zero;
+      float4_t gw = g[j] * load4(wr + 4 * c);
+      s1 += gw[0] + gw[1] + gw[2] + gw[3];
+      float4_t gx = gw * xh[j];
+      s2 += gx[0] + gx[1] + gx[2] + gx[3];
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) {
+      red[par][slot][half][0] = s1;
+      red[par][slot][half][1] = s2;
+    }
+    __syncthreads();
+    const float c1 = (red[par][slot][0][0] + red[par][slot][1][0]) * inv_d;
+    const float c2 = (red[par][slot][0][1] + red[par][slot][1][1]) * inv_d;
+#pragma unroll
+    for (int j = 0; j < HC; ++j) {
+      const int cl = lane + j * 64, c = cbase + (cl < nhalf ? cl : 0);
+      float4_t out = (g[j] * load4(wr + 4 * c) - c1 - xh[j] * c2) * rs;
+      if (dresid != nullptr) out += rr[j];
+      float4_t br = out;
+      if (dr.thr != 0) {
+        const uint64_t e0 = (uint64_t)row * d + 4 * c;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) br[t] = drop_keep(dr.seed, dr.thr, e0 + t) ? out[t] * dr.scale : 0.f;
+      }
+      pw[j] += g[j] * xh[j];  // zero past the half's end and for a dead row
+      pb[j] += g[j];
+      if (live && cl < nhalf) {
+        store4_nt(dx + row * d + 4 * c, out);
+        if (LOWP_OUT) store4(dx_lp + row * d + 4 * c, br);
+        if (has_pp) store4(pp + 4 * c, *reinterpret_cast<const float4_t*>(pp + 4 * c) + br);
+      }
+    }
+  }
+
+  // per-workgroup partial rows: dproj (already in LDS rows 2-3), then dw and db staged in rows 0-1
+  const int nacc = has_pp ? 3 : 2;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (k >= nacc) break;
+    const int which = has_pp ? (k == 0 ? 2 : k - 1) : k;
+    __syncthreads();  // dproj rows complete / previous round's readers done
+    if (which != 2) {
+#pragma unroll
+      for (int j = 0; j < HC; ++j) {
+        const int cl = lane + j * 64;
+        if (cl < nhalf) store4(smem + slot * d + 4 * (cbase + cl), which == 0 ? pw[j] : pb[j]);
+      }
+      __syncthreads();
+    }
+    const float* src = smem + (which == 2 ? 2 : 0) * d;
+    float* dst = which == 0 ? dw : (which == 1 ? db : dproj);
+    for (int col = threadIdx.x; col < d; col += blockDim.x)
+      dst[(long)blockIdx.x * d + col] = src[col] + src[d + col];
+  }
+}
+
+// LLMT_LN_BWD_SPLIT (default 1): the split-row kernel for rows wider than 768 columns; GPT-2 XL
+// same-box +0.7 % over the whole-row lean kernel (85.5k vs 84.9k tok/s, profiles/r2/ab_ln_split_xl.txt)
+inline bool ln_bwd_split(int maxc) {
+  static const int on = [] {
+    const char* e = std::getenv("LLMT_LN_BWD_SPLIT");
+    return e ? std::atoi(e) : 1;
+  }();
+  return on != 0 && maxc > 3;
+}
+
 // LLMT_LN_BWD_LEAN: rows per wave per iteration of the lean kernel (1, or 2 for rows of <= 768
 // columns; default 1); 0 = the prefetching kernel.  LLMT_LN_BWD_LEAN_WIDE=0 keeps the prefetching
 // kernel for rows wider than 768 columns (GPT-2 XL's 1600).
@@ -464,6 +594,7 @@ void launch_fwd_c(const LnFwdArgs& a, hipStream_t st) {
 // The backward kernel for this row width and LLMT_LN_BWD_LEAN setting (one signature for all)
 template <int MAXC, typename TDY, bool LP>
 auto bwd_kernel() -> decltype(&ln_bwd_kernel<MAXC, TDY, LP>) {
+  if (ln_bwd_split(MAXC)) return &ln_bwd_split_kernel<MAXC, TDY, LP>;
   switch (ln_bwd_lean_rows(MAXC)) {
     case 1: return &ln_bwd_lean_kernel<MAXC, 1, TDY, LP>;
     case 2: return &ln_bwd_lean_kernel<MAXC, MAXC <= 3 ? 2 : 1, TDY, LP>;

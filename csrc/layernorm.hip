@@ -624,10 +624,11 @@ int bwd_grid_c(const LnBwdArgs& a) {
     // columns, 1 above: GPT-2 XL d = 1600 measured 80.0k (1) vs 79.7k (4) tok/s).  More
     // than one lets the hardware dispatcher balance rows onto CUs the side stream's weight-
     // gradient GEMMs free up (124M / micro-batch 128 same-box: 1 -> 1.0224M, 2 -> 1.0259M,
-    // 4 -> 1.0276M, 8 -> 1.0243M tok/s).  The lean kernel: 3 (about the same workgroup count and
-    // column-partial traffic as 4 of the prefetching one).
+    // 4 -> 1.0276M, 8 -> 1.0243M tok/s).  The lean kernel: 1 (same box, 2 rounds: mb 32 3 / 2 / 1
+    // waves 936k / 944k / 950k tok/s, mb 128 flat; fewer partial rows for the column sums,
+    // profiles/r2/ab_ln_waves_mb*.txt).
     const char* e = std::getenv("LLMT_LN_BWD_WAVES");
-    const int waves = e ? std::max(1, std::atoi(e)) : (MAXC <= 3 ? (lean ? 3 : 4) : 1);
+    const int waves = e ? std::max(1, std::atoi(e)) : (MAXC <= 3 ? (lean ? 1 : 4) : 1);
     per_cu = (n > 0 ? n : 4) * (cus > 0 ? cus : 256) * waves;
   }
   return stride_grid((long long)(a.M + kBwdWaves - 1) / kBwdWaves, 1, per_cu);

@@ -631,7 +631,13 @@ int bwd_grid_c(const LnBwdArgs& a) {
     const int waves = e ? std::max(1, std::atoi(e)) : (MAXC <= 3 ? (lean ? 1 : 4) : 1);
     per_cu = (n > 0 ? n : 4) * (cus > 0 ? cus : 256) * waves;
   }
-  return stride_grid((long long)(a.M + kBwdWaves - 1) / kBwdWaves, 1, per_cu);
+  // LLMT_LN_BWD_MAXGRID (A/B): cap the grid, e.g. 256 = one pass of the column-sum reduction
+  static const int max_grid = [] {
+    const char* e = std::getenv("LLMT_LN_BWD_MAXGRID");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int cap = max_grid > 0 && max_grid < per_cu ? max_grid : per_cu;
+  return stride_grid((long long)(a.M + kBwdWaves - 1) / kBwdWaves, 1, cap);
 }
 
 template <int MAXC>

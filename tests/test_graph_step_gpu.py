@@ -95,3 +95,31 @@ def test_graphed_fit_checkpoint_resume(tmp_path, dropout) -> None:
     )
     assert resumed.resumed_from_step == 6 and resumed.final_step == 10
     assert abs(resumed.final_loss - full.final_loss) <= 1e-5 * abs(full.final_loss)
+
+
+def test_graphed_padded_batch_runs_eagerly(tmp_path) -> None:
+    """A batch carrying a padding mask does not fit the captured graph: that step runs eagerly
+    (through the key-padding attention path), and the following full batches replay again."""
+    import math
+
+    from llmtrain.training.trainer import Trainer
+
+    trainer = Trainer(_cfg(str(tmp_path / "p"), True))
+    batches = trainer.batch_stream()
+    for _ in range(4):  # 2 eager warm-up steps, the capture step, one replay
+        trainer.train_step(batches)
+    g = trainer._graphed
+    assert g is not None and g.replays == 2 and g.eager_steps == 2
+
+    class _Padded:
+        def next(self):
+            b = dict(batches.next())
+            mask = torch.ones_like(b["input_ids"])
+            mask[:, -5:] = 0
+            b["attention_mask"] = mask
+            return b
+
+    loss, _ = trainer.train_step(_Padded())
+    assert g.replays == 2 and g.eager_steps == 3 and math.isfinite(float(loss))
+    loss, _ = trainer.train_step(batches)
+    assert g.replays == 3 and math.isfinite(float(loss))

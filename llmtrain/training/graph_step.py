@@ -147,7 +147,7 @@ class GraphedStep:
         """One optimizer step over ``host_batches`` (the micro-batches, CPU tensors, padding masks
         already dropped where all-ones); returns ``(mean loss, pre-clip grad norm)`` as device
         scalars that later steps do not overwrite."""
-        self._stage_dropout(self._opt._step_count_host + 1)
+        self._stage_dropout(self._opt.steps_taken + 1)
         if self._calls < self._warmup or not self._graphable(host_batches):
             self._calls += 1
             self.eager_steps += 1

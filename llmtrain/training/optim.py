@@ -145,6 +145,11 @@ class FusedAdamW(torch.optim.Optimizer):
         return loss
 
 
+    @property
+    def steps_taken(self) -> int:
+        """Optimizer steps applied so far (host counter; every parameter's ``step`` in state_dict)."""
+        return self._step_count_host
+
     # -- hipGraph-captured steps (Trainer with trainer.extra.cuda_graph) --------------------
 
     def stage_graph_step(self) -> None:

@@ -59,7 +59,7 @@ def test_graphed_steps_match_eager(tmp_path) -> None:
     se, sg = eager.model.engine.store, graphed.model.engine.store
     assert torch.allclose(se.master, sg.master, rtol=0, atol=1e-6)
     oe, og = eager._optimizer, graphed._optimizer
-    assert oe._step_count_host == og._step_count_host == steps
+    assert oe.steps_taken == og.steps_taken == steps
     assert torch.allclose(oe.exp_avg_sq, og.exp_avg_sq, rtol=1e-5, atol=1e-12)
     assert eager._optimizer.param_groups[0]["lr"] == graphed._optimizer.param_groups[0]["lr"]
 

@@ -51,6 +51,15 @@ def main() -> None:
     def f32z(n):
         return torch.zeros(n, device="cuda")
 
+    from llmtrain.runtime.tuning import enable_tuned_gemms
+
+    enable_tuned_gemms(torch.device("cuda"))  # the library GEMMs exactly as the trainer issues them
+    lib_cases = {
+        "hipblaslt fwd proj (addmm)": lambda: torch.addmm(bias3[:d], x3072, w_proj.t()),
+        "hipblaslt dx fc (mm)": lambda: torch.mm(x3072, w_fc),
+        "hipblaslt dx qkv (mm)": lambda: torch.mm(x2304, w_qkv),
+        "hipblaslt fwd qkv (addmm)": lambda: torch.addmm(bias3, x768, w_qkv.t()),
+    }
     cases = {
         "fgemm fwd qkv (bias)": lambda: hip.gemm_fused(x768, w_qkv, False, 0, bias3),
         "fgemm fwd fc (bias+gelu)": lambda: hip.gemm_fused(x768, w_fc, False, 1, bias4),
@@ -89,6 +98,8 @@ def main() -> None:
         torch.cuda.synchronize()
         return out
 
+    if os.environ.get("LIB", "0") == "1":
+        cases = lib_cases
     for name, fn in cases.items():
         ref = flat(run(fn))
         bad = 0

@@ -73,6 +73,22 @@ def launch_ranks(n: int, argv: list[str]) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def summarize_buckets(steps: list[list[dict[str, float]]]) -> list[dict[str, float]]:
+    """Mean per-bucket timeline over the timed steps (FlatDataParallel.bucket_timeline rows)."""
+    if not steps:
+        return []
+    out = []
+    for i in range(len(steps[0])):
+        rows = [s[i] for s in steps if i < len(s)]
+        summary: dict[str, float] = {"bucket": i, "payload_mib": rows[0]["mib"]}
+        for key in ("ready_ms", "queue_ms", "comm_ms", "ready_to_done_ms"):
+            vals = [r[key] for r in rows if key in r]
+            if vals:
+                summary[key] = round(sum(vals) / len(vals), 3)
+        out.append(summary)
+    return out
+
+
 def make_config(args: argparse.Namespace, world: int):
     from llmtrain.config.schemas import RunConfig
 
@@ -145,6 +161,7 @@ def main() -> int:
         print(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
         return 2
     gpu = args.device == "cuda"
+    from llmtrain.parallel.comm import last_probe
     from llmtrain.parallel.dist import setup_ddp, teardown_ddp
     from llmtrain.training.trainer import Trainer
 
@@ -164,6 +181,7 @@ def main() -> int:
     rank = ddp_state.rank if ddp_state else 0
     dev = torch.device("cuda", torch.cuda.current_device()) if gpu else torch.device("cpu")
     drain = getattr(trainer.model, "drain_exposed_comm_ms", None)
+    timeline = getattr(trainer.model, "bucket_timeline", None)
 
     def barrier() -> None:
         if world > 1:
@@ -176,6 +194,8 @@ def main() -> int:
     barrier()
     if drain is not None:
         drain()
+    if timeline is not None:
+        timeline()
     t0 = time.perf_counter()
     tokens = 0
     for _ in range(args.steps):
@@ -186,6 +206,7 @@ def main() -> int:
     final_loss = float(loss.item())
     comm = drain() if drain is not None else []
     comm_ms = sum(comm) / len(comm) if comm else 0.0
+    buckets = summarize_buckets(timeline() if timeline is not None else [])
     want = args.steps * cfg.trainer.micro_batch_size * cfg.trainer.grad_accum_steps * cfg.model.block_size
     if tokens != want:  # a short data shard would silently shrink the per-GPU batch
         raise RuntimeError(f"rank {rank}: timed {tokens} tokens, expected {want}")
@@ -236,6 +257,7 @@ def main() -> int:
             "tokens_per_sec_per_gpu": round(tps / world, 1),
             "per_rank_tokens_per_sec": [round(r[1] / r[0], 1) for r in rows],
             "exposed_allreduce_ms": [round(r[2], 3) for r in rows],
+            "value_semantics": "value = aggregate tokens/s of the whole job (all ranks); per GPU: tokens_per_sec_per_gpu",
             "final_loss": round(final_loss, 4),
         }
         if gpu:
@@ -248,6 +270,15 @@ def main() -> int:
                 "tuned_gemm_table": bool(getattr(trainer, "tuned_gemms", False)),
                 "device_free_total_gib": [round(v / 2**30, 1) for v in torch.cuda.mem_get_info()],
             })
+        probe = last_probe()
+        if probe is not None:
+            result["allreduce_busbw_gbps"] = round(probe.busbw_gbps, 1)
+            result["allreduce_probe"] = {k: (round(v, 3) if isinstance(v, float) else v)
+                                         for k, v in probe.as_dict().items()}
+            for b in buckets:  # what the bucket would take alone at the probed bus bandwidth
+                b["alone_ms"] = round(b["payload_mib"] * 2**20 * 2 * (world - 1) / world / probe.busbw_gbps / 1e6, 3)
+        if buckets:
+            result["buckets_rank0"] = buckets
         print(json.dumps(result), flush=True)
     if ddp_state is not None:
         teardown_ddp()

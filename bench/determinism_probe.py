@@ -1,0 +1,100 @@
+"""Find run-to-run variation in deterministic mode, step by step, inside one process.
+
+    python bench/determinism_probe.py [--steps S] [--micro-batch B] [--reps R]
+
+For each of S optimizer steps of GPT-2 124M (``run.deterministic: true``, fused engine, side
+stream as configured by the environment) the forward + backward of that step's batch runs R times
+from the SAME weights; every repetition's loss and flat gradient buffer must equal the first bit
+for bit.  Then the optimizer steps with the last repetition's gradients and the next state is
+probed.  A mismatch names the step, the repetition and every parameter whose gradient differs —
+the kernel that produced it follows from the parameter (and the stream it ran on), which a
+whole-run comparison at step 300 cannot tell.  One JSON line per mismatch, a summary line last.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=150)
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--micro-batch", type=int, default=32)
+    ap.add_argument("--model", default="gpt2-124m")
+    ap.add_argument("--dropout", type=float, default=0.0)
+    args = ap.parse_args()
+
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_main", Path(__file__).resolve().parents[1] / "bench.py")
+    bench_mod = importlib.util.module_from_spec(spec)  # repo-root bench.py: the config builder
+    spec.loader.exec_module(bench_mod)
+    from llmtrain.training.trainer import Trainer, _to_device
+
+    ns = argparse.Namespace(
+        model=args.model, dropout=args.dropout, path="fused", device="cuda", deterministic=True,
+        micro_batch=args.micro_batch, grad_accum=1, warmup=0, steps=args.steps, bucket_mb=64.0,
+        grad_reduce_dtype="fp32", cuda_graph=False, backend="nccl",
+    )
+    torch.cuda.set_device(0)
+    cfg = bench_mod.make_config(ns, 1)
+    trainer = Trainer(cfg)
+    engine = trainer.model.engine
+    store = engine.store
+    names = {}
+    for name, p in trainer.model.named_parameters():
+        names[store.offset_of(p)] = (name, p.numel())
+    stream = trainer.batch_stream()
+    bad_total = 0
+    t0 = time.perf_counter()
+    for step in range(1, args.steps + 1):
+        batch = _to_device(stream.next(), trainer.device)
+        ref_grad = ref_loss = None
+        for rep in range(args.reps):
+            trainer.optimizer.zero_grad()
+            torch.manual_seed(1000 + step)  # the same dropout draw in every repetition
+            with trainer._policy.autocast():
+                loss, _ = trainer._adapter.compute_loss(trainer.model, batch)
+            loss.backward()
+            torch.cuda.synchronize()
+            if rep == 0:
+                ref_grad, ref_loss = store.grad.clone(), loss.detach().clone()
+                continue
+            same_loss = bool(torch.equal(loss.detach(), ref_loss))
+            if same_loss and torch.equal(store.grad, ref_grad):
+                continue
+            bad_total += 1
+            diff = store.grad != ref_grad
+            params = []
+            for off, (name, n) in sorted(names.items()):
+                cnt = int(diff[off : off + n].sum())
+                if cnt:
+                    delta = float((store.grad[off : off + n] - ref_grad[off : off + n]).abs().max())
+                    params.append({"param": name, "elems": cnt, "of": n, "max_abs": delta})
+            print(json.dumps({"step": step, "rep": rep, "loss_equal": same_loss,
+                              "loss": [float(ref_loss), float(loss)], "params": params}), flush=True)
+        trainer._optimizer_step()
+        if step % 25 == 0:
+            print(json.dumps({"progress": step, "elapsed_s": round(time.perf_counter() - t0, 1)}), flush=True)
+    torch.cuda.synchronize()
+    print(json.dumps({
+        "summary": True, "steps": args.steps, "reps": args.reps, "micro_batch": args.micro_batch,
+        "mismatches": bad_total, "wgrad_stream": os.environ.get("LLMTRAIN_WGRAD_STREAM", "1"),
+        "tuned_table": bool(getattr(trainer, "tuned_gemms", False)),
+        "master_checksum": float(store.master.double().sum()),
+    }), flush=True)
+    return 1 if bad_total else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

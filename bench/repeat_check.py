@@ -19,6 +19,11 @@ import torch
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 
+def _with(acc, fn):
+    """Run ``fn(acc)`` and return its output together with the accumulator(s) it wrote."""
+    return fn(acc), acc
+
+
 def main() -> None:
     from llmtrain import ops
     from llmtrain.ops import _ext
@@ -37,8 +42,10 @@ def main() -> None:
         return (torch.randn(*shape, device="cuda", generator=g) * scale).to(dtype)
 
     x768, x3072, x2304 = rnd(M, d), rnd(M, 4 * d), rnd(M, 3 * d)
-    w_qkv, w_fc, w_proj, w_out = rnd(3 * d, d, scale=0.02), rnd(4 * d, d, scale=0.02), rnd(d, 4 * d, scale=0.02), rnd(d, d, scale=0.02)
-    bias3, bias4 = torch.randn(3 * d, device="cuda", generator=g).to(**bf), torch.randn(4 * d, device="cuda", generator=g).to(**bf)
+    w_qkv, w_fc = rnd(3 * d, d, scale=0.02), rnd(4 * d, d, scale=0.02)
+    w_proj, w_out = rnd(d, 4 * d, scale=0.02), rnd(d, d, scale=0.02)
+    bias3 = torch.randn(3 * d, device="cuda", generator=g).to(**bf)
+    bias4 = torch.randn(4 * d, device="cuda", generator=g).to(**bf)
     u = rnd(M, 4 * d)
     qkv = rnd(M, 3 * d)
     out, lse = hip.attn_fwd(qkv, B, T, H, 0.0, 0, None)
@@ -66,13 +73,21 @@ def main() -> None:
         "fgemm fwd proj": lambda: hip.gemm_fused(x3072, w_proj, False, 0, None),
         "fgemm dx qkv": lambda: hip.gemm_fused(x2304, w_qkv, True, 0),
         "fgemm dx fc": lambda: hip.gemm_fused(x3072, w_fc, True, 0),
-        "fgemm dx proj+dgelu": lambda: (lambda db: (hip.gemm_fused(x768, w_proj, True, 2, None, u, db)[0], db))(f32z(4 * d)),
+        "fgemm dx proj+dgelu": lambda: _with(f32z(4 * d), lambda db: hip.gemm_fused(x768, w_proj, True, 2, None, u, db)[0]),
         "fgemm dx out+delta": lambda: hip.gemm_fused(dout, w_out, True, 3, None, out, f32z(d), T),
         "attn fwd": lambda: hip.attn_fwd(qkv, B, T, H, 0.0, 0, None),
-        "attn bwd": lambda: (lambda db: (hip.attn_bwd(dout, qkv, out, lse, B, T, H, 0.0, 0, db, None, None), db))(f32z(3 * d)),
-        "ln bwd": lambda: (lambda a, b, c: (hip.layernorm_bwd(dout, xs, mu, rs, w_ln, dres, a, b, None, True, c), a, b, c))(f32z(d), f32z(d), f32z(d)),
-        "wgrad fc (det slabs)": lambda: (lambda c: (hip.wgrad_gemm(u, x768, c, 0, 0, -1), c))(torch.zeros(4 * d, d, device="cuda")),
-        "wgrad qkv (det slabs)": lambda: (lambda c: (hip.wgrad_gemm(x2304, x768, c, 0, 0, -1), c))(torch.zeros(3 * d, d, device="cuda")),
+        "attn bwd": lambda: _with(
+            f32z(3 * d), lambda db: hip.attn_bwd(dout, qkv, out, lse, B, T, H, 0.0, 0, db, None, None)
+        ),
+        "ln bwd": lambda: _with(
+            (f32z(d), f32z(d), f32z(d)), lambda a: hip.layernorm_bwd(dout, xs, mu, rs, w_ln, dres, a[0], a[1], None, True, a[2])
+        ),
+        "wgrad fc (det slabs)": lambda: _with(
+            torch.zeros(4 * d, d, device="cuda"), lambda c: hip.wgrad_gemm(u, x768, c, 0, 0, -1)
+        ),
+        "wgrad qkv (det slabs)": lambda: _with(
+            torch.zeros(3 * d, d, device="cuda"), lambda c: hip.wgrad_gemm(x2304, x768, c, 0, 0, -1)
+        ),
     }
 
     def flat(o):

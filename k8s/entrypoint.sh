@@ -12,20 +12,33 @@
 #   MASTER_PORT = from the Job spec
 # Automatic recovery: every pod passes --run-id "$RUN_ID"; if the job already wrote checkpoints to
 # the shared runs PVC (a replaced pod, or the whole Job restarted) every rank resumes from the
-# newest one (data order replayed per rank, see training/trainer.py).
+# newest one (data order replayed per rank, see training/trainer.py).  The newest checkpoint and
+# the restart's run-id suffix come from `python -m llmtrain.launch` (unit-tested); the suffix is
+# the Job's UID (JOB_UID, from the pods' controller-uid label), so all ranks of one restarted gang
+# write into the same run directory.
+#
+# LAUNCH_MODE=torchrun (k8s/job-1pod8gpu.yaml): ONE pod owns all NPROC GPUs of the node and
+# torchrun starts one rank per GPU inside it — the fallback when the device plugin cannot give
+# one-GPU pods access to their peers' render nodes (RCCL would leave xGMI P2P).
 set -euo pipefail
 
-: "${JOB_COMPLETION_INDEX:?JOB_COMPLETION_INDEX is not set (not an IndexedJob?)}"
-: "${WORLD_SIZE:?WORLD_SIZE must be set}"
+: "${LAUNCH_MODE:=pod-per-gpu}"
 : "${MASTER_PORT:=29500}"
 : "${JOB_NAME:?JOB_NAME must be set}"
 : "${CONFIG_PATH:=/config/train.yaml}"
 : "${RUNS_ROOT:=/app/runs}"
 : "${RUN_ID:=${JOB_NAME}}"
-
-export RANK="$JOB_COMPLETION_INDEX"
-export LOCAL_RANK=0
 export HSA_ENABLE_IPC_MODE_LEGACY=0
+
+if [ "$LAUNCH_MODE" = torchrun ]; then
+  : "${NPROC:=8}"
+  RANK=0
+else
+  : "${JOB_COMPLETION_INDEX:?JOB_COMPLETION_INDEX is not set (not an IndexedJob?)}"
+  : "${WORLD_SIZE:?WORLD_SIZE must be set}"
+  export RANK="$JOB_COMPLETION_INDEX"
+  export LOCAL_RANK=0
+fi
 
 log() { echo "entrypoint[rank ${RANK}]: $*"; }
 
@@ -54,21 +67,31 @@ resolve_master() {
   return 1
 }
 
-MASTER_ADDR=$(resolve_master) || { echo "ERROR: could not resolve rank-0 address" >&2; exit 1; }
+if [ "$LAUNCH_MODE" = torchrun ]; then
+  MASTER_ADDR=127.0.0.1
+else
+  MASTER_ADDR=$(resolve_master) || { echo "ERROR: could not resolve rank-0 address" >&2; exit 1; }
+fi
 export MASTER_ADDR
-log "WORLD_SIZE=${WORLD_SIZE} MASTER_ADDR=${MASTER_ADDR}:${MASTER_PORT} visible GPUs: $(python -c 'import torch;print(torch.cuda.device_count())')"
+log "mode=${LAUNCH_MODE} WORLD_SIZE=${WORLD_SIZE:-$NPROC} MASTER_ADDR=${MASTER_ADDR}:${MASTER_PORT} visible GPUs: $(python -c 'import torch;print(torch.cuda.device_count())')"
 
 # newest checkpoint of this job across its run directories (the original and any restarts)
-LATEST=$(ls -1 "${RUNS_ROOT}/${RUN_ID}"*/checkpoints/step_*.pt 2>/dev/null \
-         | awk -F'step_' '{print $NF" "$0}' | sort -n | tail -n1 | cut -d' ' -f2- || true)
+LATEST=$(python -m llmtrain.launch latest-checkpoint --runs-root "$RUNS_ROOT" --run-id "$RUN_ID" || true)
 RESUME=()
 RUN_ARGS=(--run-id "$RUN_ID")
 if [ -n "$LATEST" ]; then
   RESUME=(--resume "$LATEST")
-  # a restarted job writes into a fresh run directory next to the original one
-  RUN_ARGS=(--run-id "${RUN_ID}-restart-${RESTART_TAG:-$(date +%Y%m%d%H%M%S)}")
+  # a restarted job writes into a fresh run directory next to the original one, named by the
+  # Job incarnation's UID so every rank of the gang picks the same one
+  TAG=$(python -m llmtrain.launch restart-tag) || { echo "ERROR: JOB_UID not set" >&2; exit 1; }
+  RUN_ARGS=(--run-id "${RUN_ID}-restart-${TAG}")
   log "resuming from ${LATEST}"
 fi
 
+if [ "$LAUNCH_MODE" = torchrun ]; then
+  log "exec torchrun --nproc-per-node ${NPROC} -m llmtrain train --config ${CONFIG_PATH} ${RUN_ARGS[*]} ${RESUME[*]:-}"
+  exec python -m torch.distributed.run --nnodes 1 --nproc-per-node "$NPROC" --master-addr 127.0.0.1 \
+    --master-port "$MASTER_PORT" -m llmtrain train --config "$CONFIG_PATH" "${RUN_ARGS[@]}" "${RESUME[@]}"
+fi
 log "exec python -m llmtrain train --config ${CONFIG_PATH} ${RUN_ARGS[*]} ${RESUME[*]:-}"
 exec python -m llmtrain train --config "$CONFIG_PATH" "${RUN_ARGS[@]}" "${RESUME[@]}"

@@ -10,7 +10,8 @@ validate unchanged.  The MI355X build *widens* a few literals instead of renamin
 * ``run.precision`` (new, default ``"fp32"`` = reference numerics) selects bf16 compute on GPU.
 
 New knobs that are not part of the reference contract live in the existing free-form
-``extra`` bags (``model.extra``, ``trainer.extra``, ``data.extra``).
+``extra`` bags (``model.extra``, ``trainer.extra``, ``data.extra``) and in one new bag,
+``ddp.extra`` (the startup transport checks of :mod:`llmtrain.parallel.comm`).
 """
 
 from __future__ import annotations
@@ -124,6 +125,9 @@ class DDPConfig(_Section):
     local_rank: int | None = None
     master_addr: str | None = None
     master_port: int | None = None
+    # MI355X additions (llmtrain.parallel.comm): probe_allreduce_mib, probe_iters, min_busbw_gbps,
+    # log_transport, transport_log_dir, max_channels, min_channels
+    extra: dict[str, Any] = Field(default_factory=dict)
 
 
 class MLflowConfig(_Section):

@@ -355,10 +355,11 @@ class FusedGPTEngine:
         if mask is not None:
             # key padding (no host sync: a mask is taken as given; the trainer drops all-ones masks
             # on the host before they reach the device)
-            row_w = mask.reshape(-1).float()
+            valid = mask.reshape(-1).bool()  # nonzero = valid, like the reference's mask.bool()
+            row_w = valid.float()
             row_w = row_w / row_w.sum().clamp_min(1.0)
             state.key_masks = ops.attn_key_masks(mask)
-            state.keep_col = mask.reshape(-1, 1).to(cdt)
+            state.keep_col = valid.reshape(-1, 1).to(cdt)
         else:
             row_w = torch.full((n_tok,), 1.0 / n_tok, dtype=torch.float32, device=ids.device)
 

@@ -18,6 +18,7 @@ import torch
 import torch.distributed as dist
 
 from llmtrain.config.schemas import RunConfig
+from llmtrain.parallel import comm
 
 __all__ = ["DDPState", "ReplicaMismatchError", "resolve_backend", "setup_ddp", "teardown_ddp", "verify_replicas"]
 
@@ -88,12 +89,16 @@ def setup_ddp(cfg: RunConfig) -> DDPState:
 
     backend = resolve_backend(cfg)
     kwargs = {}
+    if backend == "nccl":
+        comm.configure_rccl_env(cfg.ddp.extra, rank)
+    probe_device = torch.device("cpu")
     if _uses_gpu(cfg) and torch.cuda.is_available():
         # local_rank modulo the visible devices, as runtime/device.py picks the device: identity on a
         # full node; on a box with fewer GPUs than ranks (a gloo rehearsal of the multi-rank path)
         # ranks share devices — RCCL itself refuses two ranks on one device
         dev = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(dev)
+        probe_device = torch.device("cuda", dev)
         if backend == "nccl":
             kwargs["device_id"] = torch.device("cuda", dev)
     logger.info(
@@ -111,6 +116,8 @@ def setup_ddp(cfg: RunConfig) -> DDPState:
     )
     state = DDPState(rank=rank, world_size=world, local_rank=local, is_main=rank == 0)
     logger.info("DDP process group initialised: %s", state)
+    # startup transport check: bus bandwidth of a few large all-reduces + RCCL's transport lines
+    comm.check_transport(probe_device, cfg.ddp.extra, rank=rank)
     return state
 
 

@@ -8,8 +8,11 @@ model in ``DistributedDataParallel`` at ``training/trainer.py:86-91``; SURVEY §
   RCCL reduces in place; no bucket pack/unpack kernels, no ``gradient_as_bucket_view`` dance;
 * **overlap** — the engine calls :meth:`FlatDataParallel._on_segment_ready` as soon as a
   layer's gradients are final; when a bucket's last segment arrives its ``all_reduce`` is
-  issued asynchronously (RCCL runs it on its own stream, ordered after the producing kernels
-  by an event) while the backward of the earlier layers continues on the compute stream;
+  issued from the reducer's comm stream, ordered after the producing kernels by a stream wait,
+  while the backward of the earlier layers continues on the compute streams;
+* **observable** — per-bucket ready / start / end events (:meth:`bucket_timeline`) show how long a
+  bucket queued and how long RCCL took beside the saturating compute streams, not just the
+  exposed tail after the backward (:meth:`exposed_comm_ms`);
 * **xGMI sizing** — on a ring each GPU moves ``2(n-1)/n · S`` bytes per bucket over one link,
   so buckets are sized for link latency amortisation (default 64 MiB, two GPT-2-small blocks)
   rather than for NVSwitch;
@@ -101,6 +104,10 @@ class FlatDataParallel(nn.Module):
         self._armed = False
         self._exposed: tuple[Any, Any] | float | None = None
         self._exposed_hist: deque[tuple[Any, Any] | float] = deque(maxlen=256)
+        self._trace: list[list[Any]] = []  # this step's [bucket, ready, start, end] rows
+        self._trace_hist: deque[list[list[Any]]] = deque(maxlen=64)
+        # GPU: collectives are issued from a dedicated comm stream (see _launch)
+        self._comm = torch.cuda.Stream(device=self._store.grad.device) if self._store.grad.is_cuda else None
         engine.grad_ready = self._on_segment_ready
         if broadcast_parameters and self.world_size > 1:
             with torch.no_grad():
@@ -152,18 +159,47 @@ class FlatDataParallel(nn.Module):
             self._launch(self.buckets[idx])
 
     def _launch(self, bucket: Bucket) -> None:
+        """All-reduce one bucket.  On a GPU the collective is issued from the reducer's own comm
+        stream, which first waits for the producing stream (the engine's weight-gradient side
+        stream, already joined with the main stream): a bf16 payload is cast and cast back there,
+        so neither compute stream ever queues communication work.  Three timing events per
+        bucket — ``ready`` on the producing stream, ``start`` / ``end`` on the comm stream around
+        the collective — feed :meth:`bucket_timeline` (how long a bucket waited behind earlier
+        buckets, and how long RCCL took while the compute streams held the CUs)."""
         view = self._store.grad[bucket.start : bucket.start + bucket.numel]
-        staged = None
-        payload = view
-        if self.reduce_dtype is not None and self.reduce_dtype != view.dtype:
-            staged = view.to(self.reduce_dtype)
-            payload = staged
         op = dist.ReduceOp.AVG if self._avg_native else dist.ReduceOp.SUM
-        work = dist.all_reduce(payload, op=op, group=self._pg, async_op=True)
+        if self._comm is None:  # CPU / gloo: host timestamps; the collective runs asynchronously
+            staged = view.to(self.reduce_dtype) if self._staged_dtype(view) else None
+            payload = view if staged is None else staged
+            t_ready = time.perf_counter()
+            work = dist.all_reduce(payload, op=op, group=self._pg, async_op=True)
+            self._works.append((bucket, work, staged))
+            self._trace.append([bucket, t_ready, None, None])
+            return
+        producer = torch.cuda.current_stream()
+        ready, start, end = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        ready.record(producer)
+        self._comm.wait_stream(producer)
+        with torch.cuda.stream(self._comm):
+            start.record()
+            staged = view.to(self.reduce_dtype) if self._staged_dtype(view) else None
+            payload = view if staged is None else staged
+            work = dist.all_reduce(payload, op=op, group=self._pg, async_op=True)
+            if self._avg_native:
+                work.wait()  # RCCL: the comm stream waits for the collective (the host does not)
+                if staged is not None:
+                    view.copy_(staged)
+                end.record()
+                work = None
         self._works.append((bucket, work, staged))
+        self._trace.append([bucket, ready, start, end])
+
+    def _staged_dtype(self, view: torch.Tensor) -> bool:
+        return self.reduce_dtype is not None and self.reduce_dtype != view.dtype
 
     def finish_gradient_sync(self) -> None:
-        """Wait (stream-side on RCCL) for every launched bucket and finalise averaging.
+        """Wait for every launched bucket and finalise averaging (stream-side on RCCL: the
+        compute stream waits on the comm stream, the host does not block).
 
         The wait is bracketed by timing events on the compute stream: their distance is the
         *exposed* communication time — how long the optimizer waited for all-reduces still in
@@ -178,13 +214,21 @@ class FlatDataParallel(nn.Module):
             t_start.record()
         else:
             t_host = time.perf_counter()
-        for bucket, work, staged in self._works:
+        if self._comm is not None:
+            torch.cuda.current_stream().wait_stream(self._comm)
+        for i, (bucket, work, staged) in enumerate(self._works):
+            if work is None:
+                continue
             work.wait()
             view = self._store.grad[bucket.start : bucket.start + bucket.numel]
             if staged is not None:
                 view.copy_(staged)
             if not self._avg_native:
                 view.div_(self.world_size)
+            if on_gpu:  # gloo on GPU tensors (a rehearsal): completion seen at this wait, an upper bound
+                self._trace[i][3].record()
+            else:
+                self._trace[i][3] = time.perf_counter()
         if on_gpu:
             t_end = torch.cuda.Event(enable_timing=True)
             t_end.record()
@@ -192,8 +236,38 @@ class FlatDataParallel(nn.Module):
         else:
             self._exposed = 1000.0 * (time.perf_counter() - t_host)
         self._exposed_hist.append(self._exposed)
+        self._trace_hist.append(self._trace)
+        self._trace = []
         self._works.clear()
         self._armed = False
+
+    def bucket_timeline(self) -> list[list[dict[str, float]]]:
+        """Per synchronised step since the last call (oldest first, at most 64), per bucket:
+        ``mib`` (payload on the wire); on a GPU ``queue_ms`` (ready on the producing stream -> the comm stream started
+        it: waiting behind earlier buckets), ``comm_ms`` (start -> end: the collective itself,
+        including any wait for CUs the compute streams hold), ``ready_ms`` (ready, relative to
+        the step's first ready bucket); on the host path ``ready_to_done_ms``.  Synchronises on
+        the newest events — call at log intervals only.  Clears the history."""
+        out = []
+        wire = self.reduce_dtype or self._store.grad.dtype
+        elem = torch.empty((), dtype=wire).element_size()
+        for trace in self._trace_hist:
+            rows = []
+            first = trace[0][1] if trace else None
+            for bucket, ready, start, end in trace:
+                row: dict[str, float] = {"mib": round(bucket.numel * elem / 2**20, 2)}
+                if isinstance(ready, float):
+                    if end is not None:
+                        row["ready_to_done_ms"] = 1000.0 * (end - ready)
+                else:
+                    end.synchronize()
+                    row["ready_ms"] = float(first.elapsed_time(ready))
+                    row["queue_ms"] = float(ready.elapsed_time(start))
+                    row["comm_ms"] = float(start.elapsed_time(end))
+                rows.append(row)
+            out.append(rows)
+        self._trace_hist.clear()
+        return out
 
     def exposed_comm_ms(self) -> float | None:
         """Exposed all-reduce time of the last synchronised step in ms (``None`` before the first).

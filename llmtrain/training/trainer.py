@@ -43,6 +43,7 @@ import torch.distributed as dist
 from torch import nn
 
 from llmtrain.config.schemas import RunConfig
+from llmtrain.parallel.comm import last_probe
 from llmtrain.parallel.ddp import unwrap, wrap_data_parallel
 from llmtrain.parallel.dist import verify_replicas
 from llmtrain.parallel.dist import DDPState
@@ -104,9 +105,11 @@ def _drop_dense_mask(batch: dict[str, Any]) -> dict[str, Any]:
         and mask.device.type == "cpu"
         and mask.dtype in (torch.bool, torch.long)
         and mask.shape == ids.shape
-        and bool(mask.all())
     ):
-        return {k: v for k, v in batch.items() if k != "attention_mask"}
+        if bool(mask.all()):
+            return {k: v for k, v in batch.items() if k != "attention_mask"}
+        if not bool(mask.any()):  # reference models/gpt.py:262-266, checked here without a device sync
+            raise ValueError("attention_mask has no valid target tokens")
     return batch
 
 
@@ -206,6 +209,14 @@ class Trainer:
             async_ckpt = self._device.type == "cuda" and bool(cfg.trainer.extra.get("async_checkpoint", True))
             self._ckpt_mgr = CheckpointManager(run_dir / "checkpoints", keep_last_k=keep, async_write=async_ckpt)
         self._run_dir = run_dir
+        fail_at = cfg.trainer.extra.get("fail_at_step")
+        if fail_at is not None and int(fail_at) <= cfg.trainer.save_every_steps:
+            # the fault fires after the step's train_step and BEFORE its checkpoint: with no
+            # checkpoint on disk a restarted job would start fresh and crash again every time
+            raise ValueError(
+                f"trainer.extra.fail_at_step={fail_at} must be greater than save_every_steps="
+                f"{cfg.trainer.save_every_steps} (a restart must find a checkpoint to resume from)"
+            )
         self.last_grad_norm: torch.Tensor | None = None
         self._graphed: GraphedStep | None = None
         if bool(cfg.trainer.extra.get("cuda_graph", False)):
@@ -301,14 +312,59 @@ class Trainer:
         self._optimizer.load_state_dict(payload["optimizer_state_dict"])
         self._scheduler.load_state_dict(payload["scheduler_state_dict"])
         restore_rng_states(payload["rng_states"])
-        if self._is_ddp_active:  # the checkpoint holds rank 0's streams: split them again
-            decorrelate_rank_streams(self._rank)
+        if self._is_ddp_active:
+            ranks = (payload.get("llmtrain_extra") or {}).get("rank_rng_states")
+            if isinstance(ranks, (list, tuple)) and len(ranks) == self._world_size:
+                restore_rng_states(ranks[self._rank])  # this rank's own streams: exact continuation
+            else:  # an older checkpoint or another world size: rank 0's streams, split again
+                decorrelate_rank_streams(self._rank)
         store = getattr(self._raw_model, "flat_store", None)
         if store is not None:
             store.sync_shadow(force=True)
         step = int(payload["step"])
         logger.info("trainer: restored state from step %d", step)
         return step
+
+    def _replay_batches(self, payload: CheckpointPayload, resumed_step: int) -> int:
+        """Micro-batches this rank skips on resume so that no sample is trained twice or missed.
+
+        Same world size as the checkpoint: exactly the batches each rank had consumed.  Another
+        world size: the samplers shard one global order round-robin (``DistributedSampler``), so
+        the checkpoint's ``batches_consumed × micro_batch × world`` samples are the prefix of that
+        order already trained on; each new rank skips that many global samples' worth of its own
+        batches (rounded down, with a warning naming the samples seen again).  A checkpoint
+        without the record (reference / older files) falls back to ``step × grad_accum``."""
+        accum = self._cfg.trainer.grad_accum_steps
+        extra = payload.get("llmtrain_extra") or {}
+        saved_world, consumed = extra.get("world_size"), extra.get("batches_consumed")
+        if saved_world is None or consumed is None:
+            if self._is_ddp_active:
+                logger.warning("checkpoint: no world-size record; replaying step x grad_accum batches per rank")
+            return resumed_step * accum
+        saved_world, consumed = int(saved_world), int(consumed)
+        if saved_world == self._world_size:
+            return consumed
+        saved_mb = int(payload["config"]["trainer"]["micro_batch_size"])
+        seen = consumed * saved_mb * saved_world
+        per_batch = self._cfg.trainer.micro_batch_size * self._world_size
+        skip, again = divmod(seen, per_batch)
+        logger.warning(
+            "checkpoint: saved at world_size=%d, resuming at world_size=%d: continuing after global sample %d "
+            "(%d batches per rank; %d samples of the interrupted position are trained again)",
+            saved_world, self._world_size, seen, skip, again,
+        )
+        return skip
+
+    def _gather_rng_states(self) -> list[Any] | None:
+        """Every rank's RNG states (python / numpy / torch / HIP), gathered on the checkpoint
+        cadence so rank 0's file can restore each rank's own dropout streams."""
+        if not self._is_ddp_active:
+            return None
+        from llmtrain.training.checkpoint import capture_rng_states
+
+        states: list[Any] = [None] * self._world_size
+        dist.all_gather_object(states, capture_rng_states())
+        return states
 
     def _resolve_resume_path(self, resume_from: str | Path) -> Path:
         candidate = Path(resume_from)
@@ -481,6 +537,7 @@ class Trainer:
         batches = _Batches(self._train_loader)
         start_step = 1
         resumed_from_step: int | None = None
+        payload: Any = None
         if resume_from is not None:
             path = self._resolve_resume_path(resume_from)
             payload = CheckpointManager(path.parent, keep_last_k=1).load(path)
@@ -496,6 +553,9 @@ class Trainer:
                 )
         if self._is_main:
             self._tracker.log_params(self._cfg.model_dump())
+            probe = last_probe() if self._is_ddp_active else None
+            if probe is not None:  # the startup all-reduce probe of setup_ddp (parallel/comm.py)
+                self._tracker.log_metrics({"ddp/allreduce_busbw_gbps": probe.busbw_gbps}, step=0)
         n_params = sum(p.numel() for p in self._raw_model.parameters())
         n_trainable = sum(p.numel() for p in self._raw_model.parameters() if p.requires_grad)
 
@@ -503,7 +563,7 @@ class Trainer:
         if resumed_from_step:
             # Replay the data order: each rank skips its own shard's batches (deterministic
             # samplers), which keeps ranks aligned — the reference skips only without DDP.
-            for _ in range(resumed_from_step * accum):
+            for _ in range(self._replay_batches(payload, resumed_from_step)):
                 batches.next()
 
         first_step_loss: float | None = None
@@ -531,11 +591,13 @@ class Trainer:
             if step == 1:
                 first_step_loss = float(step_loss_dev.item())
 
-            if self._ckpt_mgr is not None and self._is_main and (step % cfg.save_every_steps == 0 or step == max_steps):
-                self._ckpt_mgr.save(
-                    step, self._raw_model, self._optimizer, self._scheduler, self._cfg,
-                    extra={"world_size": self._world_size, "batches_consumed": batches.consumed},
-                )
+            if step % cfg.save_every_steps == 0 or step == max_steps:
+                rank_rng = self._gather_rng_states()  # a collective: every rank, every save step
+                if self._ckpt_mgr is not None and self._is_main:
+                    extra = {"world_size": self._world_size, "batches_consumed": batches.consumed}
+                    if rank_rng is not None:
+                        extra["rank_rng_states"] = rank_rng
+                    self._ckpt_mgr.save(step, self._raw_model, self._optimizer, self._scheduler, self._cfg, extra=extra)
 
             interval_loss += step_loss_dev
             interval_steps += 1

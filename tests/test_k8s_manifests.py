@@ -42,11 +42,10 @@ def test_embedded_train_configs_validate() -> None:
 
 
 def test_jobs_world_size_matches_completions() -> None:
-    jobs = _docs("Job")
+    jobs = [(p, j) for p, j in _docs("Job") if j["spec"].get("completionMode") == "Indexed"]
     assert len(jobs) >= 2
     for path, job in jobs:
         spec = job["spec"]
-        assert spec["completionMode"] == "Indexed"
         env = {e["name"]: e.get("value") for e in spec["template"]["spec"]["containers"][0]["env"]}
         assert int(env["WORLD_SIZE"]) == spec["completions"] == spec["parallelism"], path
         gpu = spec["template"]["spec"]["containers"][0].get("resources", {}).get("limits", {}).get("amd.com/gpu")
@@ -121,3 +120,63 @@ def test_gang_restart_gives_up(tmp_path: Path) -> None:
     assert proc.returncode == 1
     assert "giving up after 2 restart(s)" in proc.stdout
     assert (tmp_path / "attempts").read_text().strip() == "3"
+
+
+def _env(job: dict) -> dict:
+    return {e["name"]: e for e in job["spec"]["template"]["spec"]["containers"][0]["env"]}
+
+
+def test_single_pod_fallback_job() -> None:
+    """k8s/job-1pod8gpu.yaml: one pod, all 8 GPUs, torchrun inside (docs/k8s.md fallback)."""
+    job = yaml.safe_load((ROOT / "k8s" / "job-1pod8gpu.yaml").read_text())
+    spec = job["spec"]
+    assert spec["completions"] == spec["parallelism"] == 1
+    c = spec["template"]["spec"]["containers"][0]
+    assert c["resources"]["limits"]["amd.com/gpu"] == 8
+    env = _env(job)
+    assert env["LAUNCH_MODE"]["value"] == "torchrun" and env["NPROC"]["value"] == "8"
+    vols = {v["name"] for v in spec["template"]["spec"]["volumes"]}
+    assert {"config", "runs", "mlflow", "dshm"} <= vols
+
+
+def test_jobs_share_restart_identity_and_leave_nccl_debug_to_the_trainer() -> None:
+    for path, job in _docs("Job"):
+        env = _env(job)
+        field = env["JOB_UID"]["valueFrom"]["fieldRef"]["fieldPath"]
+        assert "controller-uid" in field, path  # one value per Job incarnation, shared by its pods
+        assert "NCCL_DEBUG" not in env, path  # llmtrain.parallel.comm captures the transport lines
+
+
+def _launch(*args: str, env: dict | None = None) -> subprocess.CompletedProcess:
+    import os
+    import sys
+
+    full = dict(os.environ, PYTHONPATH=str(ROOT), **(env or {}))
+    return subprocess.run([sys.executable, "-m", "llmtrain.launch", *args], env=full, capture_output=True,
+                          text=True, timeout=120)
+
+
+def test_latest_checkpoint_across_restarts(tmp_path: Path) -> None:
+    from llmtrain.launch import latest_checkpoint
+
+    assert latest_checkpoint(tmp_path, "job") is None
+    for run, steps in {"job": [2, 4], "job-restart-ab12": [6, 10], "jobx": [99], "other": [50]}.items():
+        d = tmp_path / run / "checkpoints"
+        d.mkdir(parents=True)
+        for s in steps:
+            (d / f"step_{s:06d}.pt").write_bytes(b"x")
+    (tmp_path / "job" / "checkpoints" / "step_000012.pt.tmp").write_bytes(b"partial")  # never picked
+    assert latest_checkpoint(tmp_path, "job") == tmp_path / "job-restart-ab12" / "checkpoints" / "step_000010.pt"
+    proc = _launch("latest-checkpoint", "--runs-root", str(tmp_path), "--run-id", "job")
+    assert proc.returncode == 0 and proc.stdout.strip().endswith("job-restart-ab12/checkpoints/step_000010.pt")
+    assert _launch("latest-checkpoint", "--runs-root", str(tmp_path), "--run-id", "none").returncode == 1
+
+
+def test_restart_tag_is_shared_by_the_gang() -> None:
+    from llmtrain.launch import restart_tag
+
+    uid = "3F2A9C1E-77aa-4b1c-9d0e-123456789abc"
+    assert restart_tag({"JOB_UID": uid}) == restart_tag({"JOB_UID": uid}) == "3f2a9c1e77aa"
+    with pytest.raises(RuntimeError):
+        restart_tag({})
+    assert _launch("restart-tag", env={"JOB_UID": uid}).stdout.strip() == "3f2a9c1e77aa"

@@ -107,8 +107,11 @@ def test_tracker_injection_params_once_and_metric_steps() -> None:
 
 def test_fault_injection_and_nan_guard() -> None:
     with pytest.raises(RuntimeError, match="fault injection"):
-        Trainer(_cfg(extra={"fail_at_step": 2})).fit()
-    Trainer(_cfg(extra={"fail_at_step": 2, "fail_rank": 1})).fit()  # only rank 1 crashes
+        Trainer(_cfg(save_every_steps=1, extra={"fail_at_step": 2})).fit()
+    Trainer(_cfg(save_every_steps=1, extra={"fail_at_step": 2, "fail_rank": 1})).fit()  # only rank 1 crashes
+    # a fault before the first checkpoint would re-fire on every restart: rejected up front
+    with pytest.raises(ValueError, match="fail_at_step"):
+        Trainer(_cfg(save_every_steps=2, extra={"fail_at_step": 2}))
     trainer = Trainer(_cfg(lr=1e30, max_steps=3, log_every_steps=1, max_grad_norm=1e30))
     with pytest.raises(FloatingPointError):
         trainer.fit()

@@ -198,12 +198,10 @@ hipError_t launch_adamw_flat(const AdamWArgs& a, hipStream_t stream) {
   s.step_size = per_step[1];
   s.bc2_sqrt = per_step[2];
   s.eps = a.eps;
-  static const int tiled = [] {
-    const char* e = std::getenv("LLMT_ADAMW_TILED");  // default on: 0.75-0.78 -> 0.60 ms for 124M params
-    return e ? std::atoi(e) : 1;
-  }();
+  // tiled kernel (0.75-0.78 -> 0.60 ms for 124M params); the grid-stride kernel takes sizes that
+  // are not a multiple of 4
   const long n4 = (long)(a.n >> 2);
-  if (tiled && n4 > 0 && (a.n & 3) == 0) {
+  if (n4 > 0 && (a.n & 3) == 0) {
     const long blocks = (n4 + 511) / 512;
     if (a.shadow_bf16)
       hipLaunchKernelGGL(adamw_tiled_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, a.param, a.grad,

@@ -443,9 +443,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   };
 
   BWD_PROBE(0);
-#ifdef LLMT_BWD_SETPRIO
-  if (wave >= kBwdWaves / 2) __builtin_amdgcn_s_setprio(1);  // A/B: static priority for the younger half
-#endif
   load_tile(kblk0);
   store_tile(0);
   __syncthreads();

@@ -64,10 +64,10 @@ struct Vec8<float> {
   }
 };
 
-// OCC: waves per SIMD the register budget is sized for (6 = 3 rows per CU at 80 VGPRs; 5 = 2 rows
-// per CU at 96, no spill of the row's last vector now that all of a row's loads are in flight)
-template <int MAXV, typename T, int OCC = 6>
-__global__ __launch_bounds__(kCeThreads, OCC) void ce_fwd_bwd_kernel(
+// register budget sized for 6 waves per SIMD (3 rows per CU at 80 VGPRs; 2 rows per CU measured
+// no better, git history)
+template <int MAXV, typename T>
+__global__ __launch_bounds__(kCeThreads, 6) void ce_fwd_bwd_kernel(
     T* __restrict__ logits, const int64_t* __restrict__ labels, const float* __restrict__ row_w,
     float* __restrict__ loss, int Vp, int V) {
   __shared__ float scratch[kCeWaves];
@@ -162,15 +162,6 @@ hipError_t launch_t(T* logits, const int64_t* labels, const float* row_w, float*
     hipLaunchKernelGGL((ce_fwd_bwd_kernel<N, T>), grid, block, 0, st, logits, labels, row_w, loss, \
                        Vp, V);                                                                   \
     break;
-  // LLMT_CE_OCC=5 (A/B): the 13-vector (GPT-2 vocabulary) kernel at 2 rows per CU
-  static const int occ = [] {
-    const char* e = std::getenv("LLMT_CE_OCC");
-    return e ? std::atoi(e) : 6;
-  }();
-  if (maxv == 13 && occ == 5) {
-    hipLaunchKernelGGL((ce_fwd_bwd_kernel<13, T, 5>), grid, block, 0, st, logits, labels, row_w, loss, Vp, V);
-    return hipGetLastError();
-  }
   switch (maxv) {
     CE_CASE(1) CE_CASE(2) CE_CASE(4) CE_CASE(8) CE_CASE(13) CE_CASE(16) CE_CASE(26) CE_CASE(32)
     default: {

@@ -63,22 +63,10 @@ __device__ __forceinline__ void st8(void* base, long i8, const float* f) {
   }
 }
 
-template <bool BF16>
-__global__ __launch_bounds__(256) void gelu_fwd_kernel(const void* __restrict__ u, void* __restrict__ g,
-                                                       long n8) {
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
-    float f[8];
-    ld8<BF16>(u, i, f);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) f[k] = gelu(f[k]);
-    st8<BF16>(g, i, f);
-  }
-}
-
 // GELU forward, one tile of 4 x 256 vectors per workgroup (no grid stride): each thread issues its
 // four 16-byte loads before the first wait and the grid is large enough that the dispatcher keeps
-// every CU full (LLMT_GELU_TILED=0 restores the grid-stride kernel; solo at 131072 x 3072 bf16:
-// 0.335 -> 0.279 ms, 4.8 -> 5.8 TB/s, profiles/r2/gelu_tiled_ab.txt)
+// every CU full (vs the earlier grid-stride kernel, solo at 131072 x 3072 bf16: 0.335 -> 0.279 ms,
+// 4.8 -> 5.8 TB/s, profiles/r2/gelu_tiled_ab.txt)
 template <bool BF16>
 __global__ __launch_bounds__(256) void gelu_fwd_tiled_kernel(const void* __restrict__ u, void* __restrict__ g,
                                                              long n8) {
@@ -273,20 +261,11 @@ int rows_per_block_for(int M) {
 hipError_t launch_gelu_fwd(const void* u, void* g, bool bf16, long long n, hipStream_t stream) {
   if (n % 8 != 0) return hipErrorInvalidValue;
   const long n8 = n / 8;
-  static const int tiled = [] {
-    const char* e = std::getenv("LLMT_GELU_TILED");  // default on: 0.335 -> 0.279 ms at 131072 x 3072
-    return e ? std::atoi(e) : 1;
-  }();
-  if (tiled) {
-    const long blocks = (n8 + 1023) / 1024;
-    if (blocks > 0x7fffffffL) return hipErrorInvalidValue;
-    if (bf16) hipLaunchKernelGGL(gelu_fwd_tiled_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, u, g, n8);
-    else hipLaunchKernelGGL(gelu_fwd_tiled_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, u, g, n8);
-    return hipGetLastError();
-  }
-  const int grid = stride_grid(n8, 256, 256 * 16);
-  if (bf16) hipLaunchKernelGGL(gelu_fwd_kernel<true>, dim3(grid), dim3(256), 0, stream, u, g, n8);
-  else hipLaunchKernelGGL(gelu_fwd_kernel<false>, dim3(grid), dim3(256), 0, stream, u, g, n8);
+  // tiled kernel: 0.335 (grid-stride) -> 0.279 ms at 131072 x 3072
+  const long blocks = (n8 + 1023) / 1024;
+  if (blocks > 0x7fffffffL) return hipErrorInvalidValue;
+  if (bf16) hipLaunchKernelGGL(gelu_fwd_tiled_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, u, g, n8);
+  else hipLaunchKernelGGL(gelu_fwd_tiled_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, u, g, n8);
   return hipGetLastError();
 }
 

@@ -354,20 +354,7 @@ namespace {
 // the launcher's plan (split, tile): shared by the launch and the deterministic workspace query
 hipError_t plan_wgrad(int lda, int ldb, int M, int N, int K, int split, int tile, wgrad::Plan& p) {
   if (lda % 8 || ldb % 8 || K % 8 || lda < N) return hipErrorInvalidValue;
-  if (tile == 0) {
-    static const int forced = [] {
-      const char* e = std::getenv("LLMT_WGRAD_TILE");
-      return e ? std::atoi(e) : 0;
-    }();
-    tile = forced;
-  }
-  // LLMT_WGRAD_CUS: plan the split for fewer CUs than the chip has, leaving room for the main
-  // stream's kernels when the weight gradients run on the side stream (A/B knob)
-  static const int cus_env = [] {
-    const char* e = std::getenv("LLMT_WGRAD_CUS");
-    return e ? std::atoi(e) : 0;
-  }();
-  const int ncu = cus_env > 0 ? cus_env : gemm::cu_count();
+  const int ncu = gemm::cu_count();
   // 32-bit buffer offsets: one M chunk of either operand must stay below 2 GiB (wide rows such
   // as the LM head's 50304-column logits force a minimum split)
   const long long row_bytes = 2LL * (lda > ldb ? lda : ldb);
@@ -407,22 +394,10 @@ hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, fl
   if (det && det_ws == nullptr) return hipErrorInvalidValue;
   float* slabs = det ? det_ws : nullptr;
   const int nwg = p.tiles * p.split;
-  // LLMT_WGRAD_PIPE (A/B runs): forces the variant for every call, else the caller's choice
-  static const int pipe_env = [] {
-    const char* e = std::getenv("LLMT_WGRAD_PIPE");
-    return e ? std::atoi(e) : -1;
-  }();
-  const int pipe = pipe_env >= 0 ? pipe_env : (pipe_req >= 0 ? pipe_req : 0);
-  // LLMT_WGRAD_DEBUG=1 (timing experiments only, wrong results): every stage re-reads stage 0,
-  // so the operand stream is L2-resident and the kernel shows its compute + LDS + issue floor
-  static const int stage_mask = [] {
-    const char* e = std::getenv("LLMT_WGRAD_DEBUG");
-    return (e && e[0] == '1') ? 0 : -1;
-  }();
-  if (p.tile == 256 && pipe == 5) {
-    hipLaunchKernelGGL(wgrad::wgrad_pipe_kernel<5>, dim3(nwg), dim3(wgrad::kThreads), 0, stream, (const bf16_raw*)dy,
-                       lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k, p.m_chunk, nwg, slabs, stage_mask);
-  } else if (p.tile == 256 && pipe != 0) {
+  // the caller picks the software-pipelined 256 tile (pipe_req > 0) for GEMMs that own the chip
+  const int pipe = pipe_req > 0 ? pipe_req : 0;
+  const int stage_mask = -1;  // (0 = every stage re-reads stage 0: a timing skeleton, never shipped)
+  if (p.tile == 256 && pipe != 0) {
     hipLaunchKernelGGL(wgrad::wgrad_pipe_kernel<4>, dim3(nwg), dim3(wgrad::kThreads), 0, stream, (const bf16_raw*)dy,
                        lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k, p.m_chunk, nwg, slabs, stage_mask);
   } else if (p.tile == 256) {

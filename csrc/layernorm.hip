@@ -119,191 +119,15 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
 
 constexpr int kBwdWaves = 4;
 
-// LLMT_LN_NT (A/B): non-temporal hints in the backward for the operands nothing else re-reads soon:
-// 1 = the saved residual-stream input xs and the incoming residual gradient (read once), 2 = also
-// the outgoing fp32 residual gradient.  The bf16 dy (just written by the dX GEMM) and dx_lp (read
-// next by the GEMMs) keep the default policy.  Same box at mb 128 (profiles/r2/ln_bwd_nt_ab.txt):
-// solo 0.320 / 0.321 / 0.298 ms, in the step 1.0626M / 1.0647M / 1.0628M tok/s — noise, so 0.
-#ifndef LLMT_LN_NT
-#define LLMT_LN_NT 0
-#endif
-__device__ __forceinline__ float4_t load4_nt(const float* p) {
-  if (LLMT_LN_NT >= 1) return __builtin_nontemporal_load(reinterpret_cast<const float4_t*>(p));
-  return *reinterpret_cast<const float4_t*>(p);
-}
-__device__ __forceinline__ void store4_nt(float* p, float4_t v) {
-  if (LLMT_LN_NT >= 2) __builtin_nontemporal_store(v, reinterpret_cast<float4_t*>(p));
-  else *reinterpret_cast<float4_t*>(p) = v;
-}
+// plain loads / stores of the fp32 operands (non-temporal hints measured as noise, git history)
+__device__ __forceinline__ float4_t load4_nt(const float* p) { return *reinterpret_cast<const float4_t*>(p); }
+__device__ __forceinline__ void store4_nt(float* p, float4_t v) { *reinterpret_cast<float4_t*>(p) = v; }
 
-// Raw (unconverted) row chunk: the next row's operands are prefetched into these registers while
-// the current row is reduced, so every wave keeps two rows of loads in flight (the reductions
-// and the dependent stores otherwise serialise one HBM round trip per row).
-template <typename T> struct Raw4;
-template <> struct Raw4<float> { typedef float4_t type; };
-template <> struct Raw4<bf16_raw> { typedef ushort4_t type; };
-template <typename T>
-__device__ __forceinline__ typename Raw4<T>::type load_raw4(const T* p) {
-  return *reinterpret_cast<const typename Raw4<T>::type*>(p);
-}
-__device__ __forceinline__ float4_t to_f4(float4_t v) { return v; }
-__device__ __forceinline__ float4_t to_f4(ushort4_t v) {
-  return float4_t{bf2f(v[0]), bf2f(v[1]), bf2f(v[2]), bf2f(v[3])};
-}
-
-template <int MAXC, typename TDY, bool LOWP_OUT>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(
-    const TDY* __restrict__ dy, const float* __restrict__ xs, const float* __restrict__ mean,
-    const float* __restrict__ rstd, const float* __restrict__ w, const float* __restrict__ dresid,
-    const float* __restrict__ dy_scale, float* __restrict__ dx, TDY* __restrict__ dx_lp,
-    float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dproj, int M, int d, DropoutArgs dr) {
-  resolve_dropout(dr);
-  extern __shared__ __attribute__((aligned(16))) float smem[];  // [kBwdWaves][d], reused per accumulator
-  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nc = d >> 2;
-  const float scale = dy_scale != nullptr ? *dy_scale : 1.f;
-  const float inv_d = 1.f / (float)d;
-  // prefetching doubles the live operand registers: only for rows of <= 768 columns
-  constexpr bool kPrefetch = MAXC <= 3;
-
-  float4_t pw[MAXC], pb[MAXC], pp[MAXC];
-  float4_t wv[MAXC];
-#pragma unroll
-  for (int j = 0; j < MAXC; ++j) {
-    pw[j] = 0.f; pb[j] = 0.f; pp[j] = 0.f;
-    const int c = lane + j * 64;
-    wv[j] = c < nc ? load4(w + 4 * c) : float4_t{0.f, 0.f, 0.f, 0.f};
-  }
-
-  const long stride = (long)gridDim.x * kBwdWaves;
-  long row = (long)blockIdx.x * kBwdWaves + wid;
-  typename Raw4<TDY>::type ng[MAXC];
-  float4_t nx[MAXC];
-  float nmu = 0.f, nrs = 0.f;
-  if (kPrefetch && row < M) {
-    nmu = mean[row];
-    nrs = rstd[row];
-#pragma unroll
-    for (int j = 0; j < MAXC; ++j) {
-      const int c = lane + j * 64;
-      if (c < nc) {
-        ng[j] = load_raw4(dy + row * d + 4 * c);
-        nx[j] = load4_nt(xs + row * d + 4 * c);
-      }
-    }
-  }
-  for (; row < M; row += stride) {
-    float mu, rs;
-    float4_t g[MAXC], xh[MAXC], rr[MAXC];
-    if (kPrefetch) {
-      mu = nmu;
-      rs = nrs;
-#pragma unroll
-      for (int j = 0; j < MAXC; ++j) {
-        g[j] = to_f4(ng[j]);
-        xh[j] = nx[j];
-      }
-    } else {
-      mu = mean[row];
-      rs = rstd[row];
-#pragma unroll
-      for (int j = 0; j < MAXC; ++j) {
-        const int c = lane + j * 64;
-        if (c < nc) {
-          g[j] = load4(dy + row * d + 4 * c);
-          xh[j] = load4_nt(xs + row * d + 4 * c);
-        }
-      }
-    }
-    if (dresid != nullptr) {
-#pragma unroll
-      for (int j = 0; j < MAXC; ++j) {
-        const int c = lane + j * 64;
-        if (c < nc) rr[j] = load4_nt(dresid + row * d + 4 * c);
-      }
-    }
-    if (kPrefetch) {
-      const long nrow = row + stride;
-      if (nrow < M) {
-        nmu = mean[nrow];
-        nrs = rstd[nrow];
-#pragma unroll
-        for (int j = 0; j < MAXC; ++j) {
-          const int c = lane + j * 64;
-          if (c < nc) {
-            ng[j] = load_raw4(dy + nrow * d + 4 * c);
-            nx[j] = load4_nt(xs + nrow * d + 4 * c);
-          }
-        }
-      }
-    }
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int j = 0; j < MAXC; ++j) {
-      const int c = lane + j * 64;
-      if (c < nc) {
-        g[j] = g[j] * scale;
-        xh[j] = (xh[j] - mu) * rs;
-        float4_t gw = g[j] * wv[j];
-        s1 += gw[0] + gw[1] + gw[2] + gw[3];
-        float4_t gx = gw * xh[j];
-        s2 += gx[0] + gx[1] + gx[2] + gx[3];
-      }
-    }
-    const float c1 = wave_sum(s1) * inv_d, c2 = wave_sum(s2) * inv_d;
-#pragma unroll
-    for (int j = 0; j < MAXC; ++j) {
-      const int c = lane + j * 64;
-      if (c < nc) {
-        float4_t out = (g[j] * wv[j] - c1 - xh[j] * c2) * rs;
-        if (dresid != nullptr) out += rr[j];
-        store4_nt(dx + row * d + 4 * c, out);
-        // the branch that fed this residual stream sees its dropout mask (forward: add_ln_fwd)
-        float4_t br = out;
-        if (dr.thr != 0) {
-          const uint64_t e0 = (uint64_t)row * d + 4 * c;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) br[t] = drop_keep(dr.seed, dr.thr, e0 + t) ? out[t] * dr.scale : 0.f;
-        }
-        if (LOWP_OUT) store4(dx_lp + row * d + 4 * c, br);
-        pw[j] += g[j] * xh[j];
-        pb[j] += g[j];
-        pp[j] += br;
-      }
-    }
-  }
-
-  // Cross-wave reduction of the column partials, then this workgroup's partial row of each
-  // accumulator (dw, db, dproj point at [gridDim.x][d] partial-row buffers; the launcher sums the
-  // rows in a fixed order — reproducible, and cheaper than an atomic per column per workgroup).  One
-  // [kBwdWaves][d] buffer is reused for the 2-3 accumulators in turn: 3x less LDS than a buffer
-  // per accumulator (25.6 KB instead of 77 KB at d = 1600), so more workgroups fit on a CU.
-  const int nacc = dproj != nullptr ? 3 : 2;
-#pragma unroll
-  for (int which = 0; which < 3; ++which) {
-    if (which >= nacc) break;
-    if (which > 0) __syncthreads();  // previous round's readers are done with the buffer
-#pragma unroll
-    for (int j = 0; j < MAXC; ++j) {
-      const int c = lane + j * 64;
-      if (c < nc) store4(smem + wid * d + 4 * c, which == 0 ? pw[j] : (which == 1 ? pb[j] : pp[j]));
-    }
-    __syncthreads();
-    float* dst = which == 0 ? dw : (which == 1 ? db : dproj);
-    for (int col = threadIdx.x; col < d; col += blockDim.x) {
-      float acc = 0.f;
-#pragma unroll
-      for (int wv2 = 0; wv2 < kBwdWaves; ++wv2) acc += smem[wv2 * d + col];
-      dst[(long)blockIdx.x * d + col] = acc;
-    }
-  }
-}
-
-// Lean backward (every row width).  Same math as ln_bwd_kernel, built for latency
-// hiding rather than for the fewest instructions:
+// Lean backward (rows of <= 768 columns; the split-row kernel below takes wider rows), built for
+// latency hiding rather than for the fewest instructions:
 //  * every load is unconditional (lanes past the row end read column 0 and are zeroed): a load
 //    under a divergent `if` gets its own vmcnt(0) at the branch join, which serialised each row
-//    into one HBM round trip per 256-column chunk in the prefetching kernel;
+//    into one HBM round trip per 256-column chunk in the earlier prefetching kernel;
 //  * ROWS rows per wave per iteration, all their loads issued before the first reduction;
 //  * the dproj column partial in this wave's own LDS row instead of registers (12 KB per
 //    workgroup; per-wave rows keep the summation order fixed, i.e. deterministic), gamma re-read
@@ -549,33 +373,6 @@ __global__ __launch_bounds__(256, 3) void ln_bwd_split_kernel(
   }
 }
 
-// LLMT_LN_BWD_SPLIT (default 1): the split-row kernel for rows wider than 768 columns; GPT-2 XL
-// same-box +0.7 % over the whole-row lean kernel (85.5k vs 84.9k tok/s, profiles/r2/ab_ln_split_xl.txt)
-inline bool ln_bwd_split(int maxc) {
-  static const int on = [] {
-    const char* e = std::getenv("LLMT_LN_BWD_SPLIT");
-    return e ? std::atoi(e) : 1;
-  }();
-  return on != 0 && maxc > 3;
-}
-
-// LLMT_LN_BWD_LEAN: rows per wave per iteration of the lean kernel (1, or 2 for rows of <= 768
-// columns; default 1); 0 = the prefetching kernel.  LLMT_LN_BWD_LEAN_WIDE=0 keeps the prefetching
-// kernel for rows wider than 768 columns (GPT-2 XL's 1600).
-inline int ln_bwd_lean_rows(int maxc) {
-  static const int rows = [] {
-    const char* e = std::getenv("LLMT_LN_BWD_LEAN");
-    const int v = e ? std::atoi(e) : 1;
-    return v < 0 ? 0 : (v > 2 ? 2 : v);
-  }();
-  static const bool wide = [] {
-    const char* e = std::getenv("LLMT_LN_BWD_LEAN_WIDE");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return (maxc <= 3 || wide) ? rows : 0;
-}
-inline bool ln_bwd_lean(int maxc) { return ln_bwd_lean_rows(maxc) > 0; }
-
 template <int MAXC>
 void launch_fwd_c(const LnFwdArgs& a, hipStream_t st) {
   dim3 grid((a.M + kLnWaves - 1) / kLnWaves), block(256);
@@ -591,15 +388,13 @@ void launch_fwd_c(const LnFwdArgs& a, hipStream_t st) {
 #undef LN_FWD
 }
 
-// The backward kernel for this row width and LLMT_LN_BWD_LEAN setting (one signature for all)
+// The backward kernel for this row width: the split-row kernel above 768 columns (GPT-2 XL
+// same-box +0.7 % over the whole-row lean kernel, profiles/r2/ab_ln_split_xl.txt), else the lean
+// kernel with one row per wave per iteration (two measured no better, git history)
 template <int MAXC, typename TDY, bool LP>
-auto bwd_kernel() -> decltype(&ln_bwd_kernel<MAXC, TDY, LP>) {
-  if (ln_bwd_split(MAXC)) return &ln_bwd_split_kernel<MAXC, TDY, LP>;
-  switch (ln_bwd_lean_rows(MAXC)) {
-    case 1: return &ln_bwd_lean_kernel<MAXC, 1, TDY, LP>;
-    case 2: return &ln_bwd_lean_kernel<MAXC, MAXC <= 3 ? 2 : 1, TDY, LP>;
-    default: return &ln_bwd_kernel<MAXC, TDY, LP>;
-  }
+auto bwd_kernel() -> decltype(&ln_bwd_split_kernel<MAXC, TDY, LP>) {
+  if (MAXC > 3) return &ln_bwd_split_kernel<MAXC, TDY, LP>;
+  return &ln_bwd_lean_kernel<MAXC, 1, TDY, LP>;
 }
 
 template <int MAXC>
@@ -613,30 +408,17 @@ int bwd_grid_c(const LnBwdArgs& a) {
     int n = 0, dev = 0, cus = 0;
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const bool lean = ln_bwd_lean(MAXC);
     if (a.dy_bf16)
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, a.dx_lp ? bwd_kernel<MAXC, bf16_raw, true>()
                                                               : bwd_kernel<MAXC, bf16_raw, false>(), 256, shm);
     else
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, a.dx_lp ? bwd_kernel<MAXC, float, true>()
                                                               : bwd_kernel<MAXC, float, false>(), 256, shm);
-    // LLMT_LN_BWD_WAVES: resident waves of workgroups per launch (A/B knob; default 4 for rows of <= 768
-    // columns, 1 above: GPT-2 XL d = 1600 measured 80.0k (1) vs 79.7k (4) tok/s).  More
-    // than one lets the hardware dispatcher balance rows onto CUs the side stream's weight-
-    // gradient GEMMs free up (124M / micro-batch 128 same-box: 1 -> 1.0224M, 2 -> 1.0259M,
-    // 4 -> 1.0276M, 8 -> 1.0243M tok/s).  The lean kernel: 1 (same box, 2 rounds: mb 32 3 / 2 / 1
-    // waves 936k / 944k / 950k tok/s, mb 128 flat; fewer partial rows for the column sums,
-    // profiles/r2/ab_ln_waves_mb*.txt).
-    const char* e = std::getenv("LLMT_LN_BWD_WAVES");
-    const int waves = e ? std::max(1, std::atoi(e)) : (MAXC <= 3 ? (lean ? 1 : 4) : 1);
-    per_cu = (n > 0 ? n : 4) * (cus > 0 ? cus : 256) * waves;
+    // one resident wave of workgroups (mb 32: 1 / 2 / 3 waves 950k / 944k / 936k tok/s, fewer
+    // partial rows for the column sums; mb 128 flat: profiles/r2/ab_ln_waves_mb*.txt)
+    per_cu = (n > 0 ? n : 4) * (cus > 0 ? cus : 256);
   }
-  // LLMT_LN_BWD_MAXGRID (A/B): cap the grid, e.g. 256 = one pass of the column-sum reduction
-  static const int max_grid = [] {
-    const char* e = std::getenv("LLMT_LN_BWD_MAXGRID");
-    return e ? std::atoi(e) : 0;
-  }();
-  const int cap = max_grid > 0 && max_grid < per_cu ? max_grid : per_cu;
+  const int cap = per_cu;
   return stride_grid((long long)(a.M + kBwdWaves - 1) / kBwdWaves, 1, cap);
 }
 

@@ -115,11 +115,6 @@ class _StepState:
     muf: torch.Tensor | None = None
     rsf: torch.Tensor | None = None
     dlogits: torch.Tensor | None = None
-    # row-chunked LM head (FusedGPTEngine._head_chunked): dhf = dlogits @ W formed in the forward,
-    # the unscaled head weight gradient (side stream) and the chunk buffers / events it reads
-    dhf: torch.Tensor | None = None
-    head_dw: torch.Tensor | None = None
-    head_hold: Any = None
     drop_p: float = 0.0
     drop_seed: int = 0
     # key-padding mask (reference gpt.py:60-64, 73-74): the attention kernels' key masks and the
@@ -193,7 +188,6 @@ class FusedGPTEngine:
         # per-forward dropout base seed provider (None: one draw from torch's CPU generator)
         self.drop_seed_source: Callable[[], int] | None = None
         self._anchor = torch.zeros((), requires_grad=True, device=self.store.device)
-        self.wgrad_impl = os.environ.get("LLMTRAIN_WGRAD", "hip")
         # weight-gradient GEMMs on a second HIP stream, overlapping the dX GEMMs and the
         # bandwidth-bound backward kernels of the main stream (LLMTRAIN_WGRAD_STREAM=0 disables)
         self.wgrad_stream_enabled = os.environ.get("LLMTRAIN_WGRAD_STREAM", "1") != "0"
@@ -201,28 +195,11 @@ class FusedGPTEngine:
         # output projections (forward and dX), the fc forward with bias + GELU in its epilogue, the
         # MLP projection dX with the GELU backward + fc-bias gradient in its epilogue
         # (LLMTRAIN_FUSED_GEMM=0: hipBLASLt everywhere + separate GELU passes)
-        mode = os.environ.get("LLMTRAIN_FUSED_GEMM", "1")
-        self.fused_gemm = mode != "0"  # forward GEMMs
-        self.fused_gemm_bwd = mode not in ("0", "fwd")  # dX GEMMs
+        self.fused_gemm = os.environ.get("LLMTRAIN_FUSED_GEMM", "1") != "0"
         self.markers = os.environ.get("LLMTRAIN_ROCTX", "0") == "1" and self.store.device.type == "cuda"
         self._side: torch.cuda.Stream | None = None
         self._pending: list[torch.Tensor] = []  # operands of side-stream GEMMs of the current block
-        # A/B knob: block weight gradients (proj, fc, out, qkv) whose side-stream GEMM waits until
-        # the main stream has queued the next dX GEMM / LayerNorm backward (see _backward_blocks)
-        self.wgrad_defer = frozenset(filter(None, os.environ.get("LLMTRAIN_WGRAD_DEFER", "").split(",")))
-        self._deferred: list[tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = []
         self._held: list[tuple[Any, list[torch.Tensor]]] = []  # (side event, operands) per block
-        # LM-head weight gradient on the side stream (LLMTRAIN_HEAD_WGRAD_SIDE=1; same-box A/B: no gain,
-        # the 5 ms GEMM and the block kernels it would overlap both want the whole chip)
-        self.head_wgrad_side = os.environ.get("LLMTRAIN_HEAD_WGRAD_SIDE", "0") == "1"
-        # A/B knob: LLMTRAIN_HEAD_SCALE_FUSED=0 restores the three-pass torch rescale of hf
-        self.fused_head_scale = os.environ.get("LLMTRAIN_HEAD_SCALE_FUSED", "1") != "0"
-        # rows per LM-head chunk (0 = whole micro-batch, the default; -1 = automatic): the memory mode
-        # of _head_chunked.  Same-box at micro-batch 128 it costs 3 % (1.021M vs 1.053M tok/s,
-        # profiles/r2/head_chunk_ab.txt): the per-chunk dX GEMM (M = 16K, N = 768, K = 50304) runs
-        # 3x slower than its share of the whole one while the side stream's chunk weight gradient
-        # holds the CUs — both are compute-bound, so the overlap buys nothing
-        self.head_chunk_rows = int(os.environ.get("LLMTRAIN_HEAD_CHUNK_ROWS", "0"))
 
     # ------------------------------------------------------------------------------------
 
@@ -236,40 +213,23 @@ class FusedGPTEngine:
     def _g(self, p: torch.Tensor) -> torch.Tensor:
         return self.store.grad_of(p)
 
-    def _wgrad(self, dst: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, *, name: str = "") -> None:
+    def _wgrad(self, dst: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
         """Block weight gradients: the split-K MFMA kernel (``ops.wgrad_accum``) on GPU — it fills
-        the chip on these M-deep reductions where hipBLASLt picks too few tiles — unless
-        ``LLMTRAIN_WGRAD=hipblaslt`` selects the library GEMM for A/B runs.  On GPU it runs on the
-        side stream after an event on the main stream (``dy``/``x`` are ready); the engine holds
-        ``dy``/``x`` until the main stream has fenced the GEMM (:meth:`_retire_block`), so their
-        memory is not reused before the side stream is done with it."""
+        the chip on these M-deep reductions where hipBLASLt picks too few tiles.  On GPU it runs
+        on the side stream after an event on the main stream (``dy``/``x`` are ready); the engine
+        holds ``dy``/``x`` until the main stream has fenced the GEMM (:meth:`_retire_block`), so
+        their memory is not reused before the side stream is done with it."""
         if not (dst.is_cuda and dy.dtype == torch.bfloat16):
             accumulate_wgrad(dst, dy, x)
             return
         side = self._side_stream()
-        if side is not None and name in self.wgrad_defer:
-            self._deferred.append((dst, dy, x))  # released at the next _release_wgrads()
-            self._pending.extend((dy, x))
-        elif side is not None:
+        if side is not None:
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
-                self._wgrad_now(dst, dy, x)
+                ops.wgrad_accum(dst, dy, x)
             self._pending.extend((dy, x))
         else:
-            self._wgrad_now(dst, dy, x)
-
-    def _release_wgrads(self) -> None:
-        """Start the deferred weight gradients (LLMTRAIN_WGRAD_DEFER) on the side stream behind
-        everything the main stream has queued so far."""
-        if not self._deferred:
-            return
-        side = self._side_stream()
-        assert side is not None
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for dst, dy, x in self._deferred:
-                self._wgrad_now(dst, dy, x)
-        self._deferred = []
+            ops.wgrad_accum(dst, dy, x)
 
     def _retire_block(self) -> None:
         """End of one block's backward: fence its side-stream GEMMs with an event and release the
@@ -289,12 +249,6 @@ class FusedGPTEngine:
         while len(self._held) > self.SIDE_LAG:
             old, _ = self._held.pop(0)
             torch.cuda.current_stream().wait_event(old)
-
-    def _wgrad_now(self, dst: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, exclusive: bool = False) -> None:
-        if self.wgrad_impl == "hip":
-            ops.wgrad_accum(dst, dy, x, exclusive=exclusive)
-        else:
-            accumulate_wgrad(dst, dy, x)
 
     def _side_stream(self) -> torch.cuda.Stream | None:
         if not self.wgrad_stream_enabled or not self.store.device.type == "cuda":
@@ -398,74 +352,15 @@ class FusedGPTEngine:
             x, delta, m.ln_f.weight, m.ln_f.bias, self.eps, cdt, dropout=state.site(3 * n_layers)
         )
         head = self.store.shadow_of(self.head_weight, padded=True)
-        rows = self._head_chunk_rows(n_tok) if hf.is_cuda else 0
-        if rows:
-            loss = self._head_chunked(state, hf, head, labels.reshape(-1), row_w, rows, keep)
-        else:
-            logits = torch.mm(hf, head.t())  # [M, Vp]
-            per_row = ops.cross_entropy_fwd_bwd(logits, labels.reshape(-1), self.vocab, row_w)
-            loss = torch.dot(per_row, row_w)
-            if keep:
-                state.dlogits = logits
+        logits = torch.mm(hf, head.t())  # [M, Vp]
+        per_row = ops.cross_entropy_fwd_bwd(logits, labels.reshape(-1), self.vocab, row_w)
+        loss = torch.dot(per_row, row_w)
+        if keep:
+            state.dlogits = logits
         self._pop()
         if keep:
             state.xf, state.hf, state.muf, state.rsf = xf, hf, muf, rsf
         return loss, state
-
-    def _head_chunk_rows(self, n_tok: int) -> int:
-        """Rows per LM-head chunk (0 = the whole micro-batch at once).  ``-1`` (automatic) cuts a
-        micro-batch of at least two 16K-row chunks into up to 8 (hipBLASLt's head GEMM loses ~3 %
-        at 16K rows and ~20 % at 4K, profiles/r2/head_chunk_ce.log)."""
-        if self.head_chunk_rows >= 0:
-            rows = self.head_chunk_rows
-        else:
-            rows = max(16384, -(-n_tok // 8))
-        return rows if 0 < rows < n_tok else 0
-
-    def _head_chunked(self, st, hf, head, labels, row_w, rows: int, keep: bool) -> torch.Tensor:
-        """LM head + fused cross-entropy over row chunks, the [M, Vp] logits never materialised.
-
-        Per chunk on the main stream: ``logits_c = hf_c W^T`` (hipBLASLt), the CE kernel (loss rows
-        + dlogits in place), ``dhf_c = dlogits_c W``; the weight gradient ``dW += dlogits_c^T hf_c``
-        goes to the side stream into an fp32 buffer, overlapping the next chunk's GEMM and CE, so
-        the head's backward no longer serialises ~10 ms of split-K GEMM on the main stream.  The
-        upstream gradient is unknown in the forward: LayerNorm backward applies it to ``dhf`` as
-        before, and the backward adds ``go * dW`` to the head gradient (side stream).  Two chunk
-        buffers ping-pong; the main stream waits for the side stream before reusing one.  Peak
-        memory: 2 chunks instead of the 13.2 GB logits at 128K tokens (reference gpt.py:181-184,
-        trainer cross-entropy :256-269)."""
-        n_tok, vp = hf.shape[0], head.shape[0]
-        per_row = torch.empty(n_tok, dtype=torch.float32, device=hf.device)
-        side = self._side_stream() if keep else None
-        if keep:
-            st.dhf = torch.empty_like(hf)
-            st.head_dw = torch.zeros(self.vocab, hf.shape[1], dtype=torch.float32, device=hf.device)
-        nbuf = 2 if side is not None else 1
-        bufs = [torch.empty(rows, vp, dtype=hf.dtype, device=hf.device) for _ in range(nbuf)]
-        events: list[Any] = [None] * nbuf
-        main = torch.cuda.current_stream()
-        for c, r0 in enumerate(range(0, n_tok, rows)):
-            r1 = min(n_tok, r0 + rows)
-            k = c % nbuf
-            if events[k] is not None:
-                main.wait_event(events[k])  # the side stream is done reading this buffer
-            lc = bufs[k][: r1 - r0]
-            torch.mm(hf[r0:r1], head.t(), out=lc)
-            per_row[r0:r1] = ops.cross_entropy_fwd_bwd(lc, labels[r0:r1], self.vocab, row_w[r0:r1])
-            if not keep:
-                continue
-            torch.mm(lc, head, out=st.dhf[r0:r1])
-            if side is not None:
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    self._wgrad_now(st.head_dw, lc[:, : self.vocab], hf[r0:r1])
-                events[k] = torch.cuda.Event()
-                events[k].record(side)
-            else:
-                self._wgrad_now(st.head_dw, lc[:, : self.vocab], hf[r0:r1])
-        if keep:
-            st.head_hold = bufs  # read by the side stream: released after the backward joins it
-        return torch.dot(per_row, row_w)
 
     # -- backward --------------------------------------------------------------------------
 
@@ -485,61 +380,27 @@ class FusedGPTEngine:
 
     def _backward(self, st: _StepState, grad_out: torch.Tensor) -> None:
         go = grad_out.detach().reshape(()).float()
-        if st.head_dw is not None:
-            dhf, held = self._head_chunked_bwd(st, go)
-            self._backward_blocks(st, go, dhf, held)
-            return
         dlogits = st.dlogits
         assert dlogits is not None and st.hf is not None
         head = self.store.shadow_of(self.head_weight, padded=True)
         self._push("bwd.head")
-
-        # LM head: dhf = dlogits @ W ; dW += dlogits^T @ (go * hf).  With LLMTRAIN_HEAD_WGRAD_SIDE=1
-        # the weight gradient runs on the side stream; no record_stream then (it would pin the
-        # multi-GB dlogits block past the step and force fresh allocations every step): the engine
-        # holds dlogits until the main stream has joined the side stream at the end of the backward.
+        # LM head: dhf = dlogits @ W ; dW += dlogits^T @ (go * hf), both on the main stream (the
+        # tied [V, d] gradient is also written by the embedding backward at the end: one stream)
         dhf = torch.mm(dlogits, head)
-        # one fused pass on GPU (was bf16 -> fp32, multiply, -> bf16: three passes, 0.33 ms/step)
-        if self.fused_head_scale:
-            hf_scaled = ops.scale(st.hf, go)
-        else:
-            hf_scaled = (st.hf.float() * go).to(st.hf.dtype) if st.hf.dtype != torch.float32 else st.hf * go
-        side = self._side_stream() if self.head_wgrad_side else None
-        if side is not None:
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                accumulate_wgrad(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled)
-            held = (dlogits, hf_scaled)
-        elif dlogits.is_cuda and dlogits.dtype == torch.bfloat16:
+        hf_scaled = ops.scale(st.hf, go)  # one fused pass on GPU (fp32 math, one rounding)
+        if dlogits.is_cuda and dlogits.dtype == torch.bfloat16:
             # split-K MFMA kernel: 9.78 vs 10.34 ms for hipBLASLt's fp32-output GEMM at 128K tokens
             # (bench/head_wgrad.py; N = 50257 rows inside the 50304-wide padded logits)
-            self._wgrad_now(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled, exclusive=True)
-            held = None
+            ops.wgrad_accum(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled, exclusive=True)
         else:
             accumulate_wgrad(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled)
-            held = None
         del hf_scaled
         st.dlogits = None
         del dlogits
         self._pop()
-        self._backward_blocks(st, go, dhf, held)
+        self._backward_blocks(st, go, dhf)
 
-    def _head_chunked_bwd(self, st: _StepState, go: torch.Tensor) -> tuple[torch.Tensor, Any]:
-        """Backward of :meth:`_head_chunked`: ``grad(head) += go * dW`` on the side stream behind
-        the chunks' weight-gradient GEMMs (no main-stream wait); returns ``(dhf, held)``."""
-        g = self._g(self.head_weight)
-        if self._side is not None:
-            self._side.wait_stream(torch.cuda.current_stream())  # go
-            with torch.cuda.stream(self._side):
-                g.addcmul_(st.head_dw, go)
-        else:
-            g.addcmul_(st.head_dw, go)
-        dhf = st.dhf
-        held = (st.head_hold, st.head_dw, go)
-        st.dhf = st.head_dw = st.head_hold = None
-        return dhf, held
-
-    def _backward_blocks(self, st: _StepState, go: torch.Tensor, dhf: torch.Tensor, held: Any) -> None:
+    def _backward_blocks(self, st: _StepState, go: torch.Tensor, dhf: torch.Tensor) -> None:
         """Final LayerNorm and the transformer blocks, last to first, then the embeddings."""
         m = self.model
         bsz, seqlen = st.bsz, st.seqlen
@@ -558,16 +419,15 @@ class FusedGPTEngine:
             self._push(f"bwd.block{i}")
             blk, a = self.blocks[i], st.blocks[i]
             # MLP: delta = g Wp^T + bp ; dx is d(delta) (bias grad already summed by the LN bwd)
-            self._wgrad(self._g(blk.mlp_proj.weight), dx_lp, a.g, name="proj")
-            if self.fused_gemm_bwd:  # GELU backward + fc bias grad in the dX GEMM's epilogue
+            self._wgrad(self._g(blk.mlp_proj.weight), dx_lp, a.g)
+            if self.fused_gemm:  # GELU backward + fc bias grad in the dX GEMM's epilogue
                 du = ops.linear_dx_gelu_bwd(dx_lp, self._w(blk.mlp_proj.weight), a.u, self._g(blk.mlp_fc.bias))
             else:
                 dg = torch.mm(dx_lp, self._w(blk.mlp_proj.weight))
                 du = ops.gelu_bwd(dg, a.u, self._g(blk.mlp_fc.bias))
                 del dg
-            self._wgrad(self._g(blk.mlp_fc.weight), du, a.h2, name="fc")
+            self._wgrad(self._g(blk.mlp_fc.weight), du, a.h2)
             dh2 = torch.mm(du, self._w(blk.mlp_fc.weight))
-            self._release_wgrads()
             del du
             masked = st.keep_col is not None
             dxm, dy_lp = ops.layernorm_bwd(
@@ -580,12 +440,12 @@ class FusedGPTEngine:
                 dy_lp = dy_lp * st.keep_col
                 ops.colsum_accum(dy_lp, self._g(blk.attn.out_proj.bias))
             # attention output projection
-            self._wgrad(self._g(blk.attn.out_proj.weight), dy_lp, a.att, name="out")
+            self._wgrad(self._g(blk.attn.out_proj.weight), dy_lp, a.att)
             wo = self._w(blk.attn.out_proj.weight)
             attn_drop = st.site(2 + 3 * i)
             qkv_bg = self._g(blk.attn.qkv_proj.bias)
             delta = None
-            if self.fused_gemm_bwd:
+            if self.fused_gemm:
                 # dO plus the attention backward's row constants (and, without attention dropout,
                 # the V part of the qkv-bias gradient) from one GEMM epilogue
                 # (not taken -> delta None: attn_bwd computes it and the V-bias part itself)
@@ -603,10 +463,9 @@ class FusedGPTEngine:
                 qkv_bias_grad=qkv_bg, delta=delta, key_masks=st.key_masks,
             )
             del datt
-            self._wgrad(self._g(blk.attn.qkv_proj.weight), dqkv, a.h1, name="qkv")
+            self._wgrad(self._g(blk.attn.qkv_proj.weight), dqkv, a.h1)
             wq = self._w(blk.attn.qkv_proj.weight)
-            dh1 = ops.linear_dx(dqkv, wq) if self.fused_gemm_bwd else torch.mm(dqkv, wq)
-            self._release_wgrads()
+            dh1 = ops.linear_dx(dqkv, wq) if self.fused_gemm else torch.mm(dqkv, wq)
             del dqkv
             prev_bias = self._g(self.blocks[i - 1].mlp_proj.bias) if i > 0 else None
             dx, dx_lp = ops.layernorm_bwd(
@@ -624,4 +483,3 @@ class FusedGPTEngine:
         )
         self._notify("embed")
         self._join_side()  # clip / optimizer / loss readers on the main stream see every gradient
-        del held  # the side stream's head GEMM is ordered before any reuse of these blocks

@@ -8,8 +8,6 @@ op and no silent fallback: a GPU tensor with the extension missing raises (``_ex
 
 from __future__ import annotations
 
-import os
-
 import torch
 
 from llmtrain.ops import _ext
@@ -191,17 +189,13 @@ def attn_bwd(
 # each GEMM alone is ahead of hipBLASLt at 64K: its persistent, statically scheduled 160 KiB-LDS
 # workgroups start late on CUs still draining the previous kernel.  Above this many A bytes the
 # engine stays on hipBLASLt.
-FGEMM_MAX_A_BYTES = int(os.environ.get("LLMTRAIN_FGEMM_MAX_A_MB", "64")) * 2**20
+FGEMM_MAX_A_BYTES = 64 * 2**20
 # Ops that take the fused GEMM at any A size (knob values: fwd, fwd_gelu, dx, dx_gelu).  Default
 # dx_gelu: the MLP-projection dX with GELU backward + fc-bias grad in the epilogue replaces a
 # hipBLASLt GEMM plus a full [M, 4d] read-modify pass, and wins in the whole 124M step too
 # (same-box, micro-batch 128: +0.9 %, 994.9k/995.5k vs 985.8k/986.8k tok/s); adding the plain dX
 # GEMMs (-0.4 %) or the forward GEMMs (-1.6 %) at this size loses (scripts/abn.sh).
-FGEMM_ANY_SIZE = frozenset(filter(None, os.environ.get("LLMTRAIN_FGEMM_ANY_SIZE", "dx_gelu").split(",")))
-
-
-# LLMTRAIN_ATTN_DX_FUSED=0 keeps the attention out-projection dX on the plain paths (A/B knob)
-ATTN_DX_FUSED = os.environ.get("LLMTRAIN_ATTN_DX_FUSED", "1") != "0"
+FGEMM_ANY_SIZE = frozenset({"dx_gelu"})
 
 
 def _fgemm_ok(a: torch.Tensor, k: int, n: int, *others: torch.Tensor | None, op: str = "") -> bool:
@@ -257,8 +251,7 @@ def linear_dx_attn(dy, w, att, seqlen: int, v_bias_grad=None, head_dim: int = 64
     when the GEMM is not taken (the attention backward then computes it itself, and the caller
     must leave ``v_bias_grad`` to it)."""
     if (
-        ATTN_DX_FUSED
-        and _on_gpu(dy)
+        _on_gpu(dy)
         and dy.dtype == torch.bfloat16
         and head_dim == 64  # the epilogue's per-head row dots are 64 columns wide
         and dy.shape[0] % seqlen == 0
@@ -269,11 +262,6 @@ def linear_dx_attn(dy, w, att, seqlen: int, v_bias_grad=None, head_dim: int = 64
     return torch.mm(dy, w), None
 
 
-# LLMTRAIN_WGRAD_SIDE_TILE (A/B): force the 128- or 256-wide tile for the weight gradients that share
-# the chip with the main stream (0 = the cost model's choice)
-_SIDE_WGRAD_TILE = int(os.environ.get("LLMTRAIN_WGRAD_SIDE_TILE", "0"))
-
-
 def wgrad_accum(dst, dy, x, *, exclusive: bool = False) -> None:
     """``dst (fp32 [N, K]) += dy[M, N]^T @ x[M, K]`` — split-K MFMA GEMM with atomic fp32
     accumulation on GPU (``dy`` may be a column slice with a larger row stride).  ``exclusive``:
@@ -282,7 +270,7 @@ def wgrad_accum(dst, dy, x, *, exclusive: bool = False) -> None:
     gradients keep the 332-register kernel so main-stream waves can share its CUs (with the
     pipelined one the fc-bias column sum behind them waited ~490 us per layer)."""
     if _on_gpu(dst):
-        hip_ops().wgrad_gemm(dy, x, dst, 0, 0 if exclusive else _SIDE_WGRAD_TILE, 4 if exclusive else 0)
+        hip_ops().wgrad_gemm(dy, x, dst, 0, 0, 4 if exclusive else 0)
     else:
         dst.addmm_(dy.t().float(), x.float())
 

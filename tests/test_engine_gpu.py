@@ -169,32 +169,3 @@ def test_fused_engine_mid_run_resume(gpu_device, tmp_path, dropout):
     assert resumed.resumed_from_step == 6 and resumed.final_step == 8
     print(f"resume: full {full.final_loss!r} resumed {resumed.final_loss!r}")
     assert abs(resumed.final_loss - full.final_loss) <= 1e-5 * abs(full.final_loss)
-
-
-@pytest.mark.parametrize("rows", [384, 512, 1000])
-def test_head_chunked_matches_whole(gpu_device, rows):
-    """Row-chunked LM head + CE (dW on the side stream, go applied in the backward) equals the
-    whole-micro-batch head: loss, every gradient (tied embedding included), with a loss scale
-    and a last chunk shorter than the others."""
-    ref_model = _model(gpu_device, vocab_size=50257)
-    fused = copy.deepcopy(ref_model)
-    e_ref = ref_model.prepare_runtime(compute_dtype=torch.bfloat16)
-    e_chk = fused.prepare_runtime(compute_dtype=torch.bfloat16)
-    e_ref.head_chunk_rows = 0
-    e_chk.head_chunk_rows = rows
-    ids = torch.randint(0, 50257, (4, 256), device=gpu_device)
-    labels = torch.randint(0, 50257, (4, 256), device=gpu_device)
-    outs = []
-    for model, eng in ((ref_model, e_ref), (fused, e_chk)):
-        eng.store.zero_grad()
-        loss = model.fused_loss(ids, labels)
-        (loss * 0.25).backward()
-        torch.cuda.synchronize()
-        outs.append((loss.item(), {n: p.grad.clone() for n, p in model.named_parameters()}))
-    # same math; hipBLASLt may pick other kernels (accumulation orders, bf16 roundings) for the
-    # chunk shapes, so agreement is to bf16 rounding, not bitwise
-    assert abs(outs[0][0] - outs[1][0]) < 1e-3
-    for name, g in outs[0][1].items():
-        h = outs[1][1][name]
-        rel = ((g - h).norm() / (g.norm() + 1e-12)).item()
-        assert rel < 5e-3, f"{name}: chunked vs whole relative difference {rel:.3e}"

@@ -1,6 +1,7 @@
 """Find run-to-run variation in deterministic mode, step by step, inside one process.
 
     python bench/determinism_probe.py [--steps S] [--micro-batch B] [--reps R]
+    python bench/determinism_probe.py --runs N [--steps S]      # whole runs, compared step by step
 
 For each of S optimizer steps of GPT-2 124M (``run.deterministic: true``, fused engine, side
 stream as configured by the environment) the forward + backward of that step's batch runs R times
@@ -9,6 +10,12 @@ for bit.  Then the optimizer steps with the last repetition's gradients and the 
 probed.  A mismatch names the step, the repetition and every parameter whose gradient differs —
 the kernel that produced it follows from the parameter (and the stream it ran on), which a
 whole-run comparison at step 300 cannot tell.  One JSON line per mismatch, a summary line last.
+
+``--runs N`` instead trains N fresh trainers (same seed, same data) for S steps exactly as
+``Trainer.fit`` does — no host synchronisation between steps, so the CPU runs ahead and the
+allocator sees the production free/reuse pattern — recording every step's loss and gradient norm
+on the device; the runs must agree bit for bit at every step and in the final master weights, and
+the first step where they do not is reported.
 """
 
 from __future__ import annotations
@@ -32,6 +39,7 @@ def main() -> int:
     ap.add_argument("--micro-batch", type=int, default=32)
     ap.add_argument("--model", default="gpt2-124m")
     ap.add_argument("--dropout", type=float, default=0.0)
+    ap.add_argument("--runs", type=int, default=0, help="compare N whole runs step by step instead")
     args = ap.parse_args()
 
     import importlib.util
@@ -48,6 +56,8 @@ def main() -> int:
     )
     torch.cuda.set_device(0)
     cfg = bench_mod.make_config(ns, 1)
+    if args.runs:
+        return compare_runs(cfg, args)
     trainer = Trainer(cfg)
     engine = trainer.model.engine
     store = engine.store
@@ -94,6 +104,45 @@ def main() -> int:
         "master_checksum": float(store.master.double().sum()),
     }), flush=True)
     return 1 if bad_total else 0
+
+
+def compare_runs(cfg, args: argparse.Namespace) -> int:  # type: ignore[no-untyped-def]
+    from llmtrain.training.trainer import Trainer
+
+    results = []
+    for run in range(args.runs):
+        t0 = time.perf_counter()
+        trainer = Trainer(cfg)
+        store = trainer.model.engine.store
+        stream = trainer.batch_stream()
+        losses, norms = [], []
+        for _ in range(args.steps):
+            loss, _ = trainer.train_step(stream)  # no host sync: the production issue pattern
+            losses.append(loss.detach().reshape(1))
+            norms.append(trainer.last_grad_norm.detach().reshape(1).float())
+        torch.cuda.synchronize()
+        results.append((torch.cat(losses).cpu(), torch.cat(norms).cpu(), store.master.clone()))
+        print(json.dumps({"run": run, "final_loss": float(results[-1][0][-1]), "wall_s": round(time.perf_counter() - t0, 1),
+                          "master_checksum": float(results[-1][2].double().sum())}), flush=True)
+        del trainer, store, stream
+        torch.cuda.empty_cache()
+    bad = 0
+    ref = results[0]
+    for run, (lo, no, master) in enumerate(results[1:], start=1):
+        diff = ((lo != ref[0]) | (no != ref[1])).nonzero().flatten()
+        same_master = bool(torch.equal(master, ref[2]))
+        if len(diff) or not same_master:
+            bad += 1
+        first = int(diff[0]) + 1 if len(diff) else None
+        print(json.dumps({"run": run, "first_diverging_step": first, "diverging_steps": int(len(diff)),
+                          "master_bitwise_equal": same_master,
+                          "loss_at_first": None if first is None else [float(ref[0][first - 1]), float(lo[first - 1])],
+                          "norm_at_first": None if first is None else [float(ref[1][first - 1]), float(no[first - 1])]}),
+              flush=True)
+    print(json.dumps({"summary": True, "mode": "runs", "runs": args.runs, "steps": args.steps,
+                      "micro_batch": args.micro_batch, "runs_differing": bad,
+                      "wgrad_stream": os.environ.get("LLMTRAIN_WGRAD_STREAM", "1")}), flush=True)
+    return 1 if bad else 0
 
 
 if __name__ == "__main__":

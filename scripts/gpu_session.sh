@@ -9,6 +9,7 @@
 #   bench[:MB[:ARGS]]  bench.py --gpus 1 at micro-batch MB (default 128); ARGS: extra flags, ',' for ' '
 #   prof[:MB]          rocprofv3 kernel trace of a short bench run -> OUT/kernel_stats_mbMB.txt (per step)
 #   det[:ENV]          bench/determinism_probe.py (ENV e.g. LLMTRAIN_WGRAD_STREAM=0)
+#   detruns[:ENV]      3 whole deterministic runs of DET_STEPS (400) steps, compared step by step
 #   gloo2              bench.py --gpus 2 --backend gloo on the one GPU (rehearses the 2-rank path)
 #   micro:WHAT[:ARGS]  bench/micro.py WHAT ARGS
 #   parity[:ARGS]      bench/parity.py ARGS
@@ -51,6 +52,11 @@ for step in "$@"; do
       echo "== $name"
       env ${arg} timeout -k 10 300 python -u bench/determinism_probe.py --steps 150 --reps 3 > "$OUT/$name.jsonl" 2> "$OUT/$name.err"
       rc=$?; tail -n 2 "$OUT/$name.jsonl"; [ $rc -le 1 ] || { echo "== $name FAILED rc=$rc"; tail -20 "$OUT/$name.err"; exit $rc; } ;;
+    detruns)
+      name=detruns${arg:+_${arg//[^A-Za-z0-9]/_}}
+      echo "== $name"
+      env ${arg} timeout -k 10 400 python -u bench/determinism_probe.py --runs 3 --steps ${DET_STEPS:-400} > "$OUT/$name.jsonl" 2> "$OUT/$name.err"
+      rc=$?; tail -n 4 "$OUT/$name.jsonl"; [ $rc -le 1 ] || { echo "== $name FAILED rc=$rc"; tail -20 "$OUT/$name.err"; exit $rc; } ;;
     gloo2) run gloo2 400 python -u bench.py --gpus 2 --backend gloo --steps 4 --warmup 2 --micro-batch 16 ;;
     micro) what=${arg%%:*}; rest=""; [[ "$arg" == *:* ]] && rest=${arg#*:}
       run "micro_${what}" 400 python -u bench/micro.py "$what" ${rest//,/ } ;;

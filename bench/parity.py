@@ -1,6 +1,7 @@
 """Val-loss parity: the fused MI355X engine against torch-module training of the same model.
 
     python bench/parity.py --steps 300 --micro-batch 32            # GPT-2 124M, one MI355X
+    python bench/parity.py --steps 1500 --seeds 1337,7,42            # mean +- std per path over seeds
     python bench/parity.py --model tiny --device cpu --steps 30      # plumbing check on CPU
 
 Every path trains the reference GPT architecture from the SAME seed on the SAME synthetic token
@@ -99,31 +100,51 @@ def main() -> int:
     ap.add_argument("--lr", type=float, default=3e-4)
     ap.add_argument("--warmup", type=int, default=None, help="LR warm-up steps (default: steps // 3)")
     ap.add_argument("--seed", type=int, default=1337)
+    ap.add_argument("--seeds", default="", help="comma-separated seeds: run every path per seed, report mean/std")
     ap.add_argument("--dropout", type=float, default=0.0,
                     help="model dropout; > 0 compares the fused masks with torch's dropout statistically")
     ap.add_argument("--paths", default="fused,module_bf16,module_fp32")
     ap.add_argument("--trajectory", type=int, default=0, help="print per-step losses/grad norms of N steps instead")
     args = ap.parse_args()
 
+    seeds = [int(x) for x in args.seeds.split(",") if x] or [args.seed]
     rows = []
-    for path in args.paths.split(","):
-        if path == "fused" and args.device == "cpu":
-            continue  # the fused engine is the GPU path; its CPU reference ops are covered by tests
-        rows.append(run_path(path, args))
-        print(json.dumps(rows[-1]), flush=True)
-        if torch.cuda.is_available():
-            torch.cuda.empty_cache()
+    for seed in seeds:
+        args.seed = seed
+        for path in args.paths.split(","):
+            if path == "fused" and args.device == "cpu":
+                continue  # the fused engine is the GPU path; its CPU reference ops are covered by tests
+            rows.append({**run_path(path, args), "seed": seed})
+            print(json.dumps(rows[-1]), flush=True)
+            if torch.cuda.is_available():
+                torch.cuda.empty_cache()
     if args.trajectory:
         return 0
-    oracle = next((r for r in rows if r["path"] == "module_fp32"), None)
     summary: dict = {"model": args.model, "steps": args.steps, "micro_batch": args.micro_batch, "dropout": args.dropout,
-                     "tokens": args.steps * args.micro_batch * MODELS[args.model]["block_size"]}
-    if oracle and oracle["val_loss"]:
-        for r in rows:
-            if r is not oracle and r["val_loss"] is not None:
-                summary[f"rel_gap_{r['path']}_vs_fp32"] = round((r["val_loss"] - oracle["val_loss"]) / oracle["val_loss"], 5)
+                     "seeds": seeds, "tokens_per_run": args.steps * args.micro_batch * MODELS[args.model]["block_size"]}
+    by_path: dict[str, list[float]] = {}
+    for r in rows:
+        if r.get("val_loss") is not None:
+            by_path.setdefault(r["path"], []).append(r["val_loss"])
+    for path, vals in by_path.items():
+        summary[f"val_{path}"] = _mean_std(vals)
+    oracle = {r["seed"]: r["val_loss"] for r in rows if r["path"] == "module_fp32" and r.get("val_loss")}
+    for path in by_path:
+        if path == "module_fp32":
+            continue
+        gaps = [(r["val_loss"] - oracle[r["seed"]]) / oracle[r["seed"]] for r in rows
+                if r["path"] == path and r["seed"] in oracle and r.get("val_loss") is not None]
+        if gaps:
+            summary[f"rel_gap_{path}_vs_fp32"] = _mean_std(gaps, digits=5)
     print(json.dumps({"parity_summary": summary}), flush=True)
     return 0
+
+
+def _mean_std(vals: list[float], digits: int = 5) -> dict:
+    n = len(vals)
+    mean = sum(vals) / n
+    std = (sum((v - mean) ** 2 for v in vals) / (n - 1)) ** 0.5 if n > 1 else 0.0
+    return {"mean": round(mean, digits), "std": round(std, digits), "n": n, "values": [round(v, digits) for v in vals]}
 
 
 if __name__ == "__main__":

@@ -575,24 +575,12 @@ hipError_t launch_gemm_fused(const GemmFusedArgs& g, hipStream_t stream) {
   a.tiles_m = (g.M + BM - 1) / BM;
   a.ntiles = a.tiles_m * a.tiles_n;
   const int ncu = gemm::cu_count();
-  // LLMT_FGEMM_WAVES_OF_CUS=k: at most k x #CUs workgroups (0 = one workgroup per tile, i.e. not
-  // persistent: the dispatcher balances tiles dynamically but each tile pays its pipeline fill)
-  static const int rounds_env = [] {
-    const char* e = std::getenv("LLMT_FGEMM_WAVES_OF_CUS");
-    return e ? std::atoi(e) : 1;
-  }();
-  const long long cap = rounds_env <= 0 ? (long long)a.ntiles : (long long)ncu * rounds_env;
-  a.nwg = (int)(a.ntiles < cap ? a.ntiles : cap);
-  static const int debug = [] {
-    const char* e = std::getenv("LLMT_FGEMM_DEBUG");
-    return e ? std::atoi(e) : 0;
-  }();
-  a.debug = debug;
-  static const int band_env = [] {
-    const char* e = std::getenv("LLMT_FGEMM_BAND");
-    return e ? std::atoi(e) : 0;
-  }();
-  a.band = band_env > 0 ? (band_env < a.tiles_n ? band_env : a.tiles_n) : (kBand < a.tiles_n ? kBand : a.tiles_n);
+  a.nwg = a.ntiles < ncu ? a.ntiles : ncu;  // persistent: one workgroup per CU
+  // LLMT_FGEMM_DEBUG=1 (timing runs only, wrong results): no operand DMA — the compute skeleton
+  // alone; read per launch so one process can interleave it with the real kernel
+  const char* dbg = std::getenv("LLMT_FGEMM_DEBUG");
+  a.debug = dbg ? std::atoi(dbg) : 0;
+  a.band = kBand < a.tiles_n ? kBand : a.tiles_n;
   switch (g.epilogue * 2 + (g.b_kn ? 1 : 0)) {
     case 0: launch_one<false, 0>(a, stream); break;
     case 1: launch_one<true, 0>(a, stream); break;

@@ -341,7 +341,7 @@ class FusedGPTEngine:
             else:
                 u = self._linear(h2, blk.mlp_fc)
                 g = ops.gelu_fwd(u)
-            delta = self._linear(g, blk.mlp_proj)
+            delta = self._linear(g, blk.mlp_proj, fused=True)
             x = xm
             if keep:
                 state.blocks.append(_BlockActs(xs, h1, mu1, rs1, qkv, att, lse, xm, h2, mu2, rs2, u, g))
@@ -352,7 +352,7 @@ class FusedGPTEngine:
             x, delta, m.ln_f.weight, m.ln_f.bias, self.eps, cdt, dropout=state.site(3 * n_layers)
         )
         head = self.store.shadow_of(self.head_weight, padded=True)
-        logits = torch.mm(hf, head.t())  # [M, Vp]
+        logits = ops.head_logits(hf, head)  # [M, Vp]
         per_row = ops.cross_entropy_fwd_bwd(logits, labels.reshape(-1), self.vocab, row_w)
         loss = torch.dot(per_row, row_w)
         if keep:
@@ -386,7 +386,7 @@ class FusedGPTEngine:
         self._push("bwd.head")
         # LM head: dhf = dlogits @ W ; dW += dlogits^T @ (go * hf), both on the main stream (the
         # tied [V, d] gradient is also written by the embedding backward at the end: one stream)
-        dhf = torch.mm(dlogits, head)
+        dhf = ops.head_dx(dlogits, head)
         hf_scaled = ops.scale(st.hf, go)  # one fused pass on GPU (fp32 math, one rounding)
         if dlogits.is_cuda and dlogits.dtype == torch.bfloat16:
             # split-K MFMA kernel: 9.78 vs 10.34 ms for hipBLASLt's fp32-output GEMM at 128K tokens
@@ -427,7 +427,8 @@ class FusedGPTEngine:
                 du = ops.gelu_bwd(dg, a.u, self._g(blk.mlp_fc.bias))
                 del dg
             self._wgrad(self._g(blk.mlp_fc.weight), du, a.h2)
-            dh2 = torch.mm(du, self._w(blk.mlp_fc.weight))
+            wf = self._w(blk.mlp_fc.weight)
+            dh2 = ops.linear_dx(du, wf) if self.fused_gemm else torch.mm(du, wf)
             del du
             masked = st.keep_col is not None
             dxm, dy_lp = ops.layernorm_bwd(

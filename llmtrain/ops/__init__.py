@@ -25,6 +25,8 @@ __all__ = [
     "embedding_fwd",
     "gelu_bwd",
     "gelu_fwd",
+    "head_dx",
+    "head_logits",
     "hip_ops",
     "layernorm_bwd",
     "linear_dx",
@@ -46,11 +48,18 @@ def _on_gpu(t: torch.Tensor) -> bool:
     return t.device.type == "cuda"
 
 
+_POLICY = {"gemm_all_ours": False}
+
+
 def set_deterministic(on: bool) -> bool:
     """Process-wide deterministic mode of the HIP kernels (``run.deterministic`` on GPU): the
     split-K weight-gradient GEMM and the embedding token gradient switch from float atomics to
-    fixed-order reductions (every other reduction is fixed-order always).  Returns the previous
-    setting.  The CPU reference ops are deterministic anyway."""
+    fixed-order reductions (every other reduction is fixed-order always), and EVERY forward / dX
+    GEMM runs on the hand-written kernel (csrc/gemm_fused.hip) — hipBLASLt's Stream-K solutions
+    combine partial tiles in an order that depends on which workgroups finish first, which the
+    weight-gradient side stream perturbs (bench/determinism_probe.py --runs, docs/round3.md).
+    Returns the previous setting.  The CPU reference ops are deterministic anyway."""
+    _POLICY["gemm_all_ours"] = bool(on)
     if not _ext.load():
         return False
     prev = bool(torch.ops.llmtrain_hip.get_deterministic())
@@ -203,7 +212,7 @@ def _fgemm_ok(a: torch.Tensor, k: int, n: int, *others: torch.Tensor | None, op:
     K % 64 == 0, K >= 256, N % 8 == 0, 16-byte aligned operands, A small enough (see above)."""
     if not (k % 64 == 0 and k >= 256 and n % 8 == 0):
         return False
-    if a.numel() * a.element_size() > FGEMM_MAX_A_BYTES and op not in FGEMM_ANY_SIZE:
+    if a.numel() * a.element_size() > FGEMM_MAX_A_BYTES and op not in FGEMM_ANY_SIZE and not _POLICY["gemm_all_ours"]:
         return False
     return all(t is None or t.data_ptr() % 16 == 0 for t in (a, *others))
 
@@ -231,6 +240,36 @@ def linear_dx(dy, w):
     if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy, dy.shape[1], w.shape[1], w, op="dx"):
         return hip_ops().gemm_fused(dy, w, True, 0)[0]
     return torch.mm(dy, w)
+
+
+# rows per launch of the LM-head GEMMs on the hand-written kernel: its buffer descriptors take
+# 32-bit byte offsets, and [rows, 50304] bf16 must stay below 2 GiB
+_HEAD_ROWS = 16384
+
+
+def head_logits(h, w):
+    """``logits = h @ w^T`` for the vocab-padded LM head ``w [Vp, d]``: hipBLASLt, or row chunks
+    of the hand-written GEMM when every GEMM runs on our kernels (deterministic mode)."""
+    if not (_on_gpu(h) and _POLICY["gemm_all_ours"] and h.dtype == torch.bfloat16 and _fgemm_ok(h, h.shape[1], w.shape[0], w)):
+        return torch.mm(h, w.t())
+    out = torch.empty(h.shape[0], w.shape[0], dtype=h.dtype, device=h.device)
+    for r0 in range(0, h.shape[0], _HEAD_ROWS):
+        r1 = min(h.shape[0], r0 + _HEAD_ROWS)
+        out[r0:r1] = hip_ops().gemm_fused(h[r0:r1], w, False, 0, None)[0]
+    return out
+
+
+def head_dx(dlogits, w):
+    """``dh = dlogits @ w`` (LM-head data gradient, ``w [Vp, d]``), row-chunked like
+    :func:`head_logits` on our kernel."""
+    if not (_on_gpu(dlogits) and _POLICY["gemm_all_ours"] and dlogits.dtype == torch.bfloat16
+            and _fgemm_ok(dlogits, dlogits.shape[1], w.shape[1], w)):
+        return torch.mm(dlogits, w)
+    out = torch.empty(dlogits.shape[0], w.shape[1], dtype=dlogits.dtype, device=dlogits.device)
+    for r0 in range(0, dlogits.shape[0], _HEAD_ROWS):
+        r1 = min(dlogits.shape[0], r0 + _HEAD_ROWS)
+        out[r0:r1] = hip_ops().gemm_fused(dlogits[r0:r1], w, True, 0)[0]
+    return out
 
 
 def linear_dx_gelu_bwd(dy, w, u, dbias=None):

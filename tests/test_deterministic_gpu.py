@@ -138,3 +138,40 @@ def test_fused_step_bitwise_reproducible(deterministic, dropout) -> None:
         losses.append(loss.item())
     assert losses[0] == losses[1]
     assert torch.equal(grads[0], grads[1])
+
+
+def _det_cfg():
+    from llmtrain.config.schemas import RunConfig
+
+    return RunConfig.model_validate({
+        "schema_version": 1,
+        "run": {"name": "det", "seed": 11, "device": "cuda", "precision": "bf16", "deterministic": True},
+        "model": {"name": "gpt", "vocab_size": 50257, "block_size": 1024, "d_model": 768, "n_layers": 12,
+                  "n_heads": 12, "d_ff": 3072, "dropout": 0.0},
+        "data": {"name": "synthetic_tokens", "num_workers": 0, "extra": {"train_sequences": 64, "val_sequences": 0}},
+        "trainer": {"max_steps": 50, "micro_batch_size": 8, "grad_accum_steps": 1, "lr": 6e-4, "warmup_steps": 5},
+        "ddp": {"enabled": False}, "mlflow": {"enabled": False}, "logging": {"log_to_file": False},
+        "output": {"root_dir": "/tmp/llmtrain_det_runs"},
+    })
+
+
+def test_deterministic_training_runs_are_bitwise_equal() -> None:
+    """run.deterministic with the DEFAULT engine (weight-gradient side stream on): two 50-step GPT-2
+    124M runs in one process, issued exactly like Trainer.fit (no host sync between steps), end with
+    bitwise-equal master weights and agree at every step.  Before every GEMM moved onto the
+    hand-written kernels in this mode, the first run of a process diverged from later ones
+    (hipBLASLt Stream-K beside the side stream; bench/determinism_probe.py --runs, docs/round3.md)."""
+    from llmtrain.training.trainer import Trainer
+
+    outs = []
+    for _ in range(2):
+        trainer = Trainer(_det_cfg())
+        assert trainer.model.engine.wgrad_stream_enabled
+        stream = trainer.batch_stream()
+        losses = [trainer.train_step(stream)[0].reshape(1) for _ in range(50)]
+        torch.cuda.synchronize()
+        outs.append((torch.cat(losses).cpu(), trainer.model.engine.store.master.clone()))
+        del trainer
+        torch.cuda.empty_cache()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])

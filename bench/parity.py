@@ -90,6 +90,10 @@ def run_path(path: str, args: argparse.Namespace) -> dict:
 
 
 def main() -> int:
+    import logging
+
+    # the trainer's interval lines go to stderr: a long fp32 path shows progress every steps // 5
+    logging.basicConfig(level=logging.INFO, stream=sys.stderr, format="%(asctime)s %(name)s %(message)s")
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--model", choices=sorted(MODELS), default="gpt2-124m")
     ap.add_argument("--device", default="cuda")

@@ -143,9 +143,10 @@ def fgemm_one(K: int, N: int, epi: int = 0, b_kn: bool = False, M: int = 65536, 
                       "TFLOPs": round(2.0 * M * K * N / ms / 1e9, 1)}), flush=True)
 
 
-def fgemm_ab(M: int = 131072, variants: str = "0,2", rounds: int = 3) -> None:
-    """Interleaved in-process A/B of fused-GEMM build variants selected per launch by
-    LLMT_FGEMM_DEBUG (csrc/gemm_fused.hip) on every GPT-2 124M forward/dX shape, vs hipBLASLt."""
+def fgemm_ab(M: int = 131072, variants: str = "LLMT_FGEMM_DEBUG=0", rounds: int = 3) -> None:
+    """Interleaved in-process A/B of fused-GEMM variants selected per launch by environment
+    (``NAME=VALUE`` each, read by csrc/gemm_fused.hip at every launch) on every GPT-2 124M
+    forward/dX shape (and the epilogue variants), vs hipBLASLt."""
     import os
 
     from llmtrain.ops import _ext
@@ -163,6 +164,16 @@ def fgemm_ab(M: int = 131072, variants: str = "0,2", rounds: int = 3) -> None:
             "fwd": (lambda: ops.gemm_fused(x, w, False, 0, bias), lambda: torch.addmm(bias, x, w.t())),
             "dX": (lambda: ops.gemm_fused(dy, w, True, 0), lambda: torch.mm(dy, w)),
         }
+        if name == "proj":  # the MLP projection dX with GELU backward + fc-bias grad (epilogue 2)
+            u = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            dbk = torch.zeros(K, device=dev)
+            cases["dX+dgelu"] = (lambda: ops.gemm_fused(dy, w, True, 2, None, u, dbk),
+                                 lambda: ops.gelu_bwd(torch.mm(dy, w), u, dbk))
+        if name == "out":  # the attention out-proj dX with delta + V-bias (epilogue 3)
+            att = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            dbk2 = torch.zeros(K, device=dev)
+            cases["dX+delta"] = (lambda: ops.gemm_fused(dy, w, True, 3, None, att, dbk2, 1024),
+                                 lambda: torch.mm(dy, w))
         if name == "fc":
             cases["fwd+gelu"] = (lambda: ops.gemm_fused(x, w, False, 1, bias),
                                  lambda: ops.gelu_fwd(torch.addmm(bias, x, w.t())))
@@ -171,10 +182,11 @@ def fgemm_ab(M: int = 131072, variants: str = "0,2", rounds: int = 3) -> None:
             res: dict[str, list[float]] = {}
             for _ in range(rounds):
                 for v in variants.split(","):
-                    os.environ["LLMT_FGEMM_DEBUG"] = v
+                    key, _, val = v.partition("=")
+                    os.environ[key] = val
                     res.setdefault(f"llmt[{v}]", []).append(timeit(ours, iters=10, warmup=2))
+                    os.environ.pop(key, None)
                 res.setdefault("hipblaslt", []).append(timeit(lib, iters=10, warmup=2))
-            os.environ.pop("LLMT_FGEMM_DEBUG", None)
             row = {"gemm": name, "case": cname, "M": M}
             for k, v in res.items():
                 ms = sorted(v)[len(v) // 2]
@@ -253,7 +265,8 @@ if __name__ == "__main__":
         fgemm_one(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5] == "1",
                   M=int(sys.argv[6]) if len(sys.argv) > 6 else 65536)
     if what == "fgemm_ab":  # M variants
-        fgemm_ab(int(sys.argv[2]) if len(sys.argv) > 2 else 131072, sys.argv[3] if len(sys.argv) > 3 else "0,2")
+        fgemm_ab(int(sys.argv[2]) if len(sys.argv) > 2 else 131072,
+                 sys.argv[3] if len(sys.argv) > 3 else "LLMT_FGEMM_DEBUG=0")
     if what == "fgemm":
         fgemm(int(sys.argv[2]) if len(sys.argv) > 2 else 65536)
     if what == "fgemm_head":  # LM-head shapes (K 768 fwd, K 50304 dX)

@@ -199,12 +199,15 @@ def attn_bwd(
 # workgroups start late on CUs still draining the previous kernel.  Above this many A bytes the
 # engine stays on hipBLASLt.
 FGEMM_MAX_A_BYTES = 64 * 2**20
-# Ops that take the fused GEMM at any A size (knob values: fwd, fwd_gelu, dx, dx_gelu).  Default
-# dx_gelu: the MLP-projection dX with GELU backward + fc-bias grad in the epilogue replaces a
-# hipBLASLt GEMM plus a full [M, 4d] read-modify pass, and wins in the whole 124M step too
-# (same-box, micro-batch 128: +0.9 %, 994.9k/995.5k vs 985.8k/986.8k tok/s); adding the plain dX
-# GEMMs (-0.4 %) or the forward GEMMs (-1.6 %) at this size loses (scripts/abn.sh).
-FGEMM_ANY_SIZE = frozenset({"dx_gelu"})
+# Ops that take the fused GEMM at any A size.  dx_gelu: the MLP-projection dX with GELU backward +
+# fc-bias grad in the epilogue replaces a hipBLASLt GEMM plus a full [M, 4d] read-modify pass, and
+# wins in the whole 124M step (same-box, micro-batch 128: +0.9 %, 994.9k/995.5k vs 985.8k/986.8k
+# tok/s).  dx_attn: the attention out-projection dX with the backward's delta rows and the V-bias
+# column sums in the epilogue (deletes the delta pass; same-box mb 128: 1,076.3k vs 1,074.5k tok/s,
+# profiles/r3/ab_dx_attn_any_size_mb128.txt).  Adding the plain dX GEMMs (-0.4 %) or the forward
+# GEMMs (-1.6 %) at this size loses: hipBLASLt's 256x256 kernels run 1.1-1.3 PF on these shapes
+# against 0.86-1.14 PF for ours (profiles/r3/fgemm_wide_v2_ab_m131k.log).
+FGEMM_ANY_SIZE = frozenset({"dx_gelu", "dx_attn"})
 
 
 def _fgemm_ok(a: torch.Tensor, k: int, n: int, *others: torch.Tensor | None, op: str = "") -> bool:

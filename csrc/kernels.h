@@ -146,7 +146,7 @@ long wgrad_gemm_det_ws_floats(int lda, int ldb, int M, int N, int K, int split, 
 // `pipe`: 0 = the plain 256-tile kernel (332 registers per lane: other kernels' waves can share
 // its SIMDs — the side-stream default), 4 / 5 = the software-pipelined one with that many ring
 // slots (all 512 registers: nothing else runs beside it — for GEMMs that own the chip), -1 = the
-// LLMT_WGRAD_PIPE environment default (0).
+// default (0).
 hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N,
                              int K, int split, int tile, hipStream_t stream, float* det_ws = nullptr, int pipe = -1);
 

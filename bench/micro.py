@@ -237,6 +237,11 @@ def attn(B: int = 32, T: int = 1024, H: int = 12) -> list[dict]:
     rows.append({"attn": "llmtrain fwd", "ms": round(ms, 4), "TFLOPs": round(flops_fwd / ms / 1e9, 1)})
     ms = timeit(lambda: ops.attn_bwd(dout, qkv, out, lse, B, T, H))
     rows.append({"attn": "llmtrain bwd", "ms": round(ms, 4), "TFLOPs": round(2.5 * flops_fwd / ms / 1e9, 1)})
+    # as in the training step: delta rows already formed by the out-projection dX GEMM's epilogue
+    delta = (dout.float().view(B, T, H, 64) * out.float().view(B, T, H, 64)).sum(-1).permute(0, 2, 1).contiguous()
+    ms = timeit(lambda: ops.attn_bwd(dout, qkv, out, lse, B, T, H, 0.0, 0, None, delta))
+    rows.append({"attn": "llmtrain bwd, delta ready", "ms": round(ms, 4),
+                 "TFLOPs": round(2.5 * flops_fwd / ms / 1e9, 1)})
     q, k, v = (t.transpose(1, 2).contiguous() for t in qkv.view(B, T, 3, H, 64).unbind(2))
     q.requires_grad_(True); k.requires_grad_(True); v.requires_grad_(True)
     do = dout.view(B, T, H, 64).transpose(1, 2).contiguous()

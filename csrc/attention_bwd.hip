@@ -17,12 +17,19 @@
 //    same LDS images that serve the row reads (one swizzle, conflict free both ways);
 //  * dS crosses LDS once (as a [key][q] image written 8 bytes per lane) and dQ = dS K is formed
 //    with 16x16x32 MFMAs over the block's 256 keys (K^T LDS image, one ds_read_b128 per B
-//    operand); each key block stores its dQ contribution to its OWN bf16 partial plane with
-//    plain stores (4-5x the chip-wide float-atomic rate, and no memset), and a reduce pass sums
-//    the <= T/256 planes per row straight into the packed bf16 dqkv;
-//  * branch-free buffer loads (rows past T read as zero), double-buffered Q/dO and dS images,
-//    one barrier per query tile; heaviest key blocks dispatched first, the key blocks of one
-//    (batch, head) on one XCD (shared Q/dO in its L2);
+//    operand);
+//  * work split: when B*H fills the CUs evenly (GPT-2 124M at micro-batch 128: 1,536 pairs on 256
+//    CUs), ONE workgroup per (batch, head) sweeps its key blocks in order and keeps dQ in fp32 in
+//    a private buffer — each query tile's partial is read at the top of the tile (latency under
+//    phase A) and the rows of the current key block's own 256-row band, which no later block
+//    touches, leave as bf16 straight into dqkv: no reduce pass, no bf16 partials, every
+//    workgroup the same causal work (no tail).  Otherwise (small B*H, or dropout) one workgroup
+//    per (batch, head, key block), heaviest first, each storing its dQ contribution to its own
+//    bf16 partial plane, and a reduce pass sums the <= T/256 planes per row into dqkv;
+//  * Q/dO tiles by LDS-DMA two tiles ahead into a 3-buffer ring (the register-staged version
+//    exposed one global round trip per 64-row tile), row constants one tile ahead in registers;
+//    branch-free buffer loads (rows past T read as zero), double-buffered dS images, one barrier
+//    per query tile;
 //  * measured LDS bank conflicts (rocprofv3 PMC, profiles/r2/pmc_attention_b32_after.txt): 8.9 %
 //    of LDS-active cycles at B=32 (the forward: 0).  The Q/dO row and transposed reads are
 //    conflict free by construction; the remainder is not attributed per access site (candidates:
@@ -212,30 +219,43 @@ __device__ __forceinline__ float swap_pair(float x) {
 // 16 rows a ds_read_b128 lane group touches land on 16 distinct chunks (all 64 banks)
 __device__ __forceinline__ int kt_off(int d, int key) { return d * kKvBlk + ((((key >> 3) ^ (d & 15))) << 3) + (key & 7); }
 
-template <bool DROPOUT, bool KMASK, bool SMALLHD>
+template <bool DROPOUT, bool KMASK, bool SMALLHD, bool SPLIT>
 __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __restrict__ qkv,
                                                           const bf16_raw* __restrict__ dout,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta,
-                                                          const bf16_raw* __restrict__ out_o,
                                                           bf16_raw* __restrict__ dqkv,
-                                                          float* __restrict__ dq_part, float* __restrict__ vparts,
+                                                          float* __restrict__ dq_acc, float* __restrict__ vparts,
+                                                          float* __restrict__ qparts,
                                                           int T, int H, int nkb, DropoutArgs dr, int hd_arg,
                                                           float scale_arg, const uint8_t* __restrict__ key_valid) {
   resolve_dropout(dr);
   __shared__ __attribute__((aligned(16))) bf16_raw kt_lds[kHD * kKvBlk];             // K^T, 32 KB
-  __shared__ __attribute__((aligned(16))) bf16_raw qd_lds[2][2][kQTile * kHD];      // [buf][Q|dO] 32 KB
+  __shared__ __attribute__((aligned(16))) bf16_raw qd_lds[3][2][kQTile * kHD];      // [buf][Q|dO] 48 KB
   __shared__ __attribute__((aligned(16))) bf16_raw ds_lds[2][kKvBlk * kQTile];      // [buf][key][q] 64 KB
   __shared__ __attribute__((aligned(16))) float rowc_lds[2][2 * kQTile];            // lse*log2e | delta
-  __shared__ float bias_red[kBwdWaves][kHD];                                       // V bias (dropout)
+  __shared__ float bias_red[kBwdWaves][kHD];                                       // V (dropout) / Q bias
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int half = lane >> 5, col = lane & 31;
-  // grid (B*H, nkb): chunked heaviest-first dispatch (attention_common.h chunked_dispatch); key
-  // block 0 sees the most query tiles
-  int bh, kb;
-  chunked_dispatch(bh, kb);
+  // Two work splits (template SPLIT: separate code, so the split grid keeps the leaner register
+  // allocation of a body without the fp32 accumulation):
+  //  * grid (B*H): one workgroup per (b, h) sweeps its key blocks in order and accumulates dQ in
+  //    fp32 in a private buffer (no reduce pass; every workgroup the same causal work, so no tail
+  //    as long as B*H fills the CUs evenly);
+  //  * grid (B*H, nkb) ("split", for B*H that would leave CUs idle): one workgroup per (b, h, key
+  //    block), heaviest first (attention_common.h chunked_dispatch), each key block's dQ into its
+  //    own bf16 partial plane, summed by attn_dq_reduce_kernel.
+  constexpr bool split = SPLIT;
+  int bh, kb_first;
+  if (split) {
+    chunked_dispatch(bh, kb_first);
+  } else {
+    bh = blockIdx.x;
+    kb_first = 0;
+  }
+  const int kb_end = split ? kb_first + 1 : nkb;
   const int b = bh / H, h = bh - b * H;
   const int hd = SMALLHD ? hd_arg : kHD;  // head dim in memory; tiles and fragments stay 64 wide
   const long row_stride = 3L * H * hd;
@@ -256,24 +276,22 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
                                                                          (int)((T - 1) * out_stride + hd) * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t r_lse = __builtin_amdgcn_make_buffer_rsrc((void*)lse_bh, (short)0, T * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t r_del = __builtin_amdgcn_make_buffer_rsrc((void*)delta_bh, (short)0, T * 4, 0x00020000);
-  // fused delta (out_o != nullptr): each thread also stages the O chunk matching its dO chunk and
-  // the tile's delta[r] = sum_d dO O is formed at staging time — no separate delta pass over dO and
-  // O (the 2.5x re-read of O per query row across key blocks stays in L2: a pair's key blocks share
-  // an XCD); without dropout the key block 0 workgroup (it sees every query row) also forms the
-  // column sums of dO = the V part of the qkv-bias gradient, vparts[b][h * hd + d]
-  const bool fuse_delta = out_o != nullptr;  // kernel argument: uniform
-  const __amdgpu_buffer_rsrc_t r_o = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(fuse_delta ? out_o + (long)b * T * H * hd + (long)h * hd : dobase), (short)0,
-      fuse_delta ? (int)((T - 1) * out_stride + hd) * 2 : 0, 0x00020000);
-  const bool vsum = fuse_delta && !DROPOUT && vparts != nullptr && kb == 0;
-
   const uint32_t pseed = DROPOUT ? mix32(dr.seed + (uint32_t)bh * 0x9E3779B9u) : 0u;  // see attn fwd
+  const float scale = SMALLHD ? scale_arg : 0.125f;
+  const float c = scale * 1.4426950408889634f;
+  const int ntq = (T + kQTile - 1) / kQTile;
+  const int qt_dq = wave & 3;   // dQ output rows 16*qt_dq .. of the 64-row tile
+  const int dp_dq = wave >> 2;  // dQ output cols 32*dp_dq .. (two 16-wide tiles)
+  // column sums of this lane's final dQ (columns 32 dp + (lane & 15) and + 16): the Q part of the
+  // qkv-bias gradient
+  float qsum0 = 0.f, qsum1 = 0.f;
+
+  for (int kb = kb_first; kb < kb_end; ++kb) {
+  if (kb > kb_first) __syncthreads();  // the previous key block's K^T image / LDS rings are retired
   const int kblk0 = kb * kKvBlk;
   const int kw0 = kblk0 + 32 * wave;  // first key of this wave
   const int key = kw0 + col;          // this lane's key
 
-  const float scale = SMALLHD ? scale_arg : 0.125f;
-  const float c = scale * 1.4426950408889634f;
   // key padding: this lane's key (on the MFMA lane) is excluded from P when padded
   const bool kvalid = !KMASK || (key < T && key_valid[(long)b * T + key] != 0);
 
@@ -296,57 +314,38 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
     for (int j = 0; j < 8; ++j) kt_lds[kt_off(16 * kk + 8 * half + j, 32 * wave + col)] = kv[j];
   }
 
-  // register staging of one 64-row Q/dO tile (+ its row constants): thread t holds Q and dO (and,
-  // fusing delta, O) of row (t >> 3) & 63, chunk t & 7
-  ushort8_t stg[2], stg_o;
+  // Q/dO tiles arrive by LDS-DMA two tiles ahead into a 3-buffer ring (no register staging, ~32 KB
+  // in flight per CU instead of 16: the register-staged version exposed one global round trip per
+  // tile).  Wave w moves rows 8w..8w+7 of the Q and of the dO tile, one 1-KiB op each: lane l lands
+  // at LDS byte 16 l of the op, i.e. row 8w + (l >> 3), swizzled slot l & 7, so it loads the source
+  // chunk swz(row, slot) (the swizzle is an involution); head dims past a small hd and rows past T
+  // load as zeros.
+  const int dma_row = 8 * wave + (lane >> 3);
+  const int dma_ch = swz(dma_row, lane & 7);
+  const bool dma_live = !SMALLHD || dma_ch * 8 < hd;
+  auto dma_tile = [&](int q0, int buf) {
+    const int qrow = q0 + dma_row;
+    const int oq = dma_live ? (int)(qrow * row_stride + dma_ch * 8) * 2 : kOobOff;
+    const int od = dma_live ? (int)(qrow * out_stride + dma_ch * 8) * 2 : kOobOff;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r_q, (lds_void*)&qd_lds[buf][0][8 * wave * kHD], 16, oq, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r_do, (lds_void*)&qd_lds[buf][1][8 * wave * kHD], 16, od, 0, 0, 0);
+  };
+  // row constants of a tile (lse: wave 0, delta: wave 1) through one register each, one tile ahead;
+  // a wave-uniform choice of descriptor (a per-lane select made hipcc emit a readfirstlane
+  // waterfall loop around the load)
   float stc = 0.f;
-  float vcol[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // dO column sums (vsum)
-  auto load_tile = [&](int q0) {
-    const int r = (threadIdx.x >> 3) & 63, ch = threadIdx.x & 7;
-    const int qrow = q0 + r;
-    const bool live = !SMALLHD || ch * 8 < hd;
-    stg[0] = buf_load16(r_q, live ? (int)(qrow * row_stride + ch * 8) * 2 : kOobOff);
-    stg[1] = buf_load16(r_do, live ? (int)(qrow * out_stride + ch * 8) * 2 : kOobOff);
-    if (fuse_delta) {
-      stg_o = buf_load16(r_o, live ? (int)(qrow * out_stride + ch * 8) * 2 : kOobOff);
-      if (threadIdx.x < kQTile) stc = buf_load_f32(r_lse, (q0 + threadIdx.x) * 4);
-    } else if (wave < 2) {
-      // wave 0: lse, wave 1: delta — a wave-uniform choice of descriptor (a per-lane select of the
-      // descriptor made hipcc emit a readfirstlane waterfall loop around the load, every tile)
+  auto load_rowc = [&](int q0) {
+    if (wave < 2) {
       const int qq = q0 + (threadIdx.x & (kQTile - 1));
       stc = wave == 0 ? buf_load_f32(r_lse, qq * 4) : buf_load_f32(r_del, qq * 4);
     }
   };
-  auto store_tile = [&](int buf) {
-    const int r = (threadIdx.x >> 3) & 63, ch = threadIdx.x & 7;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) *reinterpret_cast<ushort8_t*>(&qd_lds[buf][i][tile_chunk_off(r, ch)]) = stg[i];
-    if (fuse_delta) {
-      // delta[r]: this thread's 8 products, then the row's 8 threads (consecutive lanes)
-      float a[8], o[8];
-      unpack8(stg[1], a);
-      unpack8(stg_o, o);
-      float dot = 0.f;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        dot = fmaf(a[k], o[k], dot);
-        if (vsum) vcol[k] += a[k];  // rows past T load as zeros
-      }
-      dot += __shfl_xor(dot, 1, 64);
-      dot += __shfl_xor(dot, 2, 64);
-      dot += __shfl_xor(dot, 4, 64);
-      if (threadIdx.x < kQTile) rowc_lds[buf][threadIdx.x] = stc * 1.4426950408889634f;
-      if (ch == 0 && threadIdx.x < 8 * kQTile) rowc_lds[buf][kQTile + r] = dot;
-    } else if (threadIdx.x < 2 * kQTile) {
-      rowc_lds[buf][threadIdx.x] = threadIdx.x < kQTile ? stc * 1.4426950408889634f : stc;
-    }
+  auto store_rowc = [&](int buf) {
+    if (threadIdx.x < 2 * kQTile) rowc_lds[buf][threadIdx.x] = threadIdx.x < kQTile ? stc * 1.4426950408889634f : stc;
   };
 
   f32x16 dk[2], dv[2];
   dk[0] = 0.f; dk[1] = 0.f; dv[0] = 0.f; dv[1] = 0.f;
-
-  const int qt_dq = wave & 3;   // dQ output rows 16*qt_dq .. of the 64-row tile
-  const int dp_dq = wave >> 2;  // dQ output cols 32*dp_dq .. (two 16-wide tiles)
 
   // ---- phase A of one 32-row query sub-tile: S, P, dP, dS, dV^T, dK^T, dS^T image ----------
   // full: the whole 64-row tile lies below the diagonal of every key of the block and inside the
@@ -443,26 +442,48 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   };
 
   BWD_PROBE(0);
-  load_tile(kblk0);
-  store_tile(0);
+  const int ntiles = (T - kblk0 + kQTile - 1) / kQTile;
+  load_rowc(kblk0);
+  dma_tile(kblk0, 0);
+  if (ntiles > 1) dma_tile(kblk0 + kQTile, 1);
+  store_rowc(0);
+  // tile 0 landed (this wave's ops; the barrier covers the others'): tile 1's two ops may fly
+  if (ntiles > 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   BWD_PROBE(1);
 
-  int it = 0;
+  int it = 0, cur3 = 0;
   for (int q0 = kblk0; q0 < T; q0 += kQTile, ++it) {
     const int cur = it & 1;
-    const bool more = q0 + kQTile < T;
-    if (more) load_tile(q0 + kQTile);  // latency hidden under this tile's MFMAs
-    const bf16_raw* q_lds = qd_lds[cur][0];
-    const bf16_raw* do_lds = qd_lds[cur][1];
+    const bool more = it + 1 < ntiles, more2 = it + 2 < ntiles;
+    // the next tile's row constants, then the DMA of the tile after it (program order matters: the
+    // constants' own wait must not cover those two ops)
+    if (more) load_rowc(q0 + kQTile);
+    // this lane's fp32 dQ partial of the tile from the earlier key blocks (workgroup-private buffer
+    // in MFMA-fragment order: 32 contiguous bytes per lane), read now, used after phase A
+    float* accp = dq_acc + ((((long)bh * ntq + q0 / kQTile) * kBwdWaves + wave) * 64 + lane) * 8;
+    f32x4 prev0 = {0.f, 0.f, 0.f, 0.f}, prev1 = prev0;
+    if (!split && kb > 0) {
+      prev0 = *reinterpret_cast<const f32x4*>(accp);
+      prev1 = *reinterpret_cast<const f32x4*>(accp + 4);
+    }
+    const int nxt3 = cur3 == 2 ? 0 : cur3 + 1, nxt3b = nxt3 == 2 ? 0 : nxt3 + 1;
+    if (more2) dma_tile(q0 + 2 * kQTile, nxt3b);
+    const bf16_raw* q_lds = qd_lds[cur3][0];
+    const bf16_raw* do_lds = qd_lds[cur3][1];
     bf16_raw* dsimg = ds_lds[cur];
     phase_a(q0 >= kblk0 + kKvBlk && q0 + kQTile <= T, q0, q_lds, do_lds, rowc_lds[cur], dsimg);
     BWD_PROBE(2 + 3 * it);
-    if (more) store_tile(cur ^ 1);
-    // one barrier per tile: the dS image and the next Q/dO tile are double-buffered, so the only
-    // hand-off is "phase A of this tile (and the next tile's staging) done by every wave"
+    if (more) store_rowc(cur ^ 1);
+    // one barrier per tile: tile it+1's Q/dO landed (only tile it+2's two ops may still fly; the
+    // buffer they fill was last read by phase A of tile it-1, before the previous barrier), the
+    // dS image is double-buffered, so the only hand-off is "phase A of this tile done by every wave"
+    if (more2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     BWD_PROBE(3 + 3 * it);
+    cur3 = nxt3;
 
     // ---- dQ[q0 + 16 qt .., 32 dp + (0..31)] += dS K over the block's 256 keys (16x16x32) ----
     {
@@ -496,27 +517,56 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
         acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[ks], b0[ks], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[ks], b1[ks], acc1, 0, 0, 0);
       }
-      // this key block's dQ contribution -> its own bf16 partial plane (plain stores; the planes
-      // are the largest traffic of the backward: bf16 halves the bytes written here and read by
-      // attn_dq_reduce_kernel, which sums them in fp32).  Lanes i and i^1 swap half their rows so
-      // each lane stores whole dwords (two adjacent columns): even lanes rows 0,1, odd rows 2,3.
+      // dQ accumulates in fp32 across the key blocks: rows below this key block (every earlier block
+      // contributed) add the partial read at the top of the tile; rows of the block's own 256-row
+      // band get no later contribution, so they leave as bf16 straight into dqkv (scaled), all other
+      // rows go back to the private buffer.  Rows past T and dims past hd are zero (zero Q rows /
+      // masked P; zero K^T dims).
+      acc0 += prev0;
+      acc1 += prev1;
+      // lanes i and i^1 swap half their rows so each lane stores whole dwords (two adjacent
+      // columns): even lanes rows 0,1, odd rows 2,3
       const int p = i & 1;
-      const int dcol = 32 * dp_dq + (i & ~1);  // even column of this lane's pair
-      bf16_raw* plane = reinterpret_cast<bf16_raw*>(dq_part) + ((long)kb * gridDim.x + bh) * T * kHD;
+      if (split) {  // this key block's bf16 partial plane [kb][b, h, t, 64]
+        bf16_raw* plane = reinterpret_cast<bf16_raw*>(dq_acc) + ((long)kb * gridDim.x + bh) * T * kHD;
+        const int dcol = 32 * dp_dq + (i & ~1);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int r = p ? 2 + j : j;  // the row this lane stores
-        const int qq = q0 + 16 * qt_dq + 4 * g + r;
-        const float s0 = swap_pair(p ? acc0[j] : acc0[2 + j]);
-        const float s1 = swap_pair(p ? acc1[j] : acc1[2 + j]);
-        const float o0 = p ? acc0[2 + j] : acc0[j], o1 = p ? acc1[2 + j] : acc1[j];
-        const uint32_t w0 = (uint32_t)f2bf((p ? s0 : o0) * scale) | ((uint32_t)f2bf((p ? o0 : s0) * scale) << 16);
-        const uint32_t w1 = (uint32_t)f2bf((p ? s1 : o1) * scale) | ((uint32_t)f2bf((p ? o1 : s1) * scale) << 16);
-        if (qq < T) {
-          bf16_raw* dst = plane + (long)qq * kHD + dcol;
-          *reinterpret_cast<uint32_t*>(dst) = w0;
-          *reinterpret_cast<uint32_t*>(dst + 16) = w1;
+        for (int j = 0; j < 2; ++j) {
+          const int r = p ? 2 + j : j;
+          const int qq = q0 + 16 * qt_dq + 4 * g + r;
+          const float s0 = swap_pair(p ? acc0[j] : acc0[2 + j]);
+          const float s1 = swap_pair(p ? acc1[j] : acc1[2 + j]);
+          const float o0 = p ? acc0[2 + j] : acc0[j], o1 = p ? acc1[2 + j] : acc1[j];
+          const uint32_t w0 = (uint32_t)f2bf((p ? s0 : o0) * scale) | ((uint32_t)f2bf((p ? o0 : s0) * scale) << 16);
+          const uint32_t w1 = (uint32_t)f2bf((p ? s1 : o1) * scale) | ((uint32_t)f2bf((p ? o1 : s1) * scale) << 16);
+          if (qq < T) {
+            bf16_raw* dst = plane + (long)qq * kHD + dcol;
+            *reinterpret_cast<uint32_t*>(dst) = w0;
+            *reinterpret_cast<uint32_t*>(dst + 16) = w1;
+          }
         }
+      } else if (q0 >= kblk0 + kKvBlk) {
+        *reinterpret_cast<f32x4*>(accp) = acc0;
+        *reinterpret_cast<f32x4*>(accp + 4) = acc1;
+      } else {
+        const int dcol = 32 * dp_dq + (i & ~1);  // even column of this lane's pair
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int r = p ? 2 + j : j;  // the row this lane stores
+          const int qq = q0 + 16 * qt_dq + 4 * g + r;
+          const float s0 = swap_pair(p ? acc0[j] : acc0[2 + j]);
+          const float s1 = swap_pair(p ? acc1[j] : acc1[2 + j]);
+          const float o0 = p ? acc0[2 + j] : acc0[j], o1 = p ? acc1[2 + j] : acc1[j];
+          const uint32_t w0 = (uint32_t)f2bf((p ? s0 : o0) * scale) | ((uint32_t)f2bf((p ? o0 : s0) * scale) << 16);
+          const uint32_t w1 = (uint32_t)f2bf((p ? s1 : o1) * scale) | ((uint32_t)f2bf((p ? o1 : s1) * scale) << 16);
+          if (qq < T) {
+            bf16_raw* dst = dqkv + ((long)b * T + qq) * row_stride + (long)h * hd + dcol;
+            if (!SMALLHD || dcol < hd) *reinterpret_cast<uint32_t*>(dst) = w0;
+            if (!SMALLHD || dcol + 16 < hd) *reinterpret_cast<uint32_t*>(dst + 16) = w1;
+          }
+        }
+        qsum0 += (acc0[0] + acc0[1] + acc0[2] + acc0[3]) * scale;
+        qsum1 += (acc1[0] + acc1[1] + acc1[2] + acc1[3]) * scale;
       }
     }
     BWD_PROBE(4 + 3 * it);
@@ -549,41 +599,46 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   // sum this block's 256 keys of dV^T — over the 32 lanes of each half, then over the 8 waves —
   // into this block's partial row vparts[b * nkb + kb][h * hd + d].
   BWD_PROBE(63);
-  if (vsum) {  // wave-uniform (kb, kernel arguments): column sums of dO over all rows of this (b, h)
+  if (DROPOUT && vparts != nullptr) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
+    for (int dt = 0; dt < 2; ++dt) {
 #pragma unroll
-      for (int off = 8; off < 64; off <<= 1) vcol[k] += __shfl_xor(vcol[k], off, 64);
-    if (lane < 8) {
+      for (int r = 0; r < 16; ++r) {
+        float vv = dv[dt][r];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) bias_red[wave][8 * lane + k] = vcol[k];
+        for (int off = 1; off < 32; off <<= 1) vv += __shfl_xor(vv, off, 64);
+        if (col == 0) bias_red[wave][dt * 32 + 8 * (r >> 2) + 4 * half + (r & 3)] = vv;
+      }
     }
     __syncthreads();
     if (threadIdx.x < hd) {
       float acc = 0.f;
 #pragma unroll
       for (int w = 0; w < kBwdWaves; ++w) acc += bias_red[w][threadIdx.x];
-      vparts[(long)b * (H * hd) + h * hd + threadIdx.x] = acc;
+      vparts[((long)b * nkb + kb) * (H * hd) + h * hd + threadIdx.x] = acc;
     }
-    return;
   }
-  if (!DROPOUT || vparts == nullptr) return;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float vv = dv[dt][r];
-#pragma unroll
-      for (int off = 1; off < 32; off <<= 1) vv += __shfl_xor(vv, off, 64);
-      if (col == 0) bias_red[wave][dt * 32 + 8 * (r >> 2) + 4 * half + (r & 3)] = vv;
-    }
+  }  // key blocks
+
+  // Q part of the qkv-bias gradient: this (b, h)'s column sums of dQ, one partial row
+  // qparts[b][h * hd + d] (lanes of one column, then the four waves of one column half, fixed order)
+  if (split || qparts == nullptr) return;  // uniform (the split grid's Q part comes from the reduce)
+  qsum0 += __shfl_xor(qsum0, 16, 64);
+  qsum0 += __shfl_xor(qsum0, 32, 64);
+  qsum1 += __shfl_xor(qsum1, 16, 64);
+  qsum1 += __shfl_xor(qsum1, 32, 64);
+  __syncthreads();  // bias_red's V use is over
+  if (lane < 16) {
+    bias_red[wave][32 * dp_dq + lane] = qsum0;
+    bias_red[wave][32 * dp_dq + 16 + lane] = qsum1;
   }
   __syncthreads();
   if (threadIdx.x < hd) {
+    const int dp = threadIdx.x >> 5;
     float acc = 0.f;
 #pragma unroll
-    for (int w = 0; w < kBwdWaves; ++w) acc += bias_red[w][threadIdx.x];
-    vparts[((long)b * nkb + kb) * (H * hd) + h * hd + threadIdx.x] = acc;
+    for (int qt = 0; qt < 4; ++qt) acc += bias_red[qt + 4 * dp][threadIdx.x];
+    qparts[(long)b * (H * hd) + h * hd + threadIdx.x] = acc;
   }
 }
 
@@ -888,8 +943,17 @@ int bwd_plane_width(int hd) { return hd == 2 * attn::kHD ? 2 * attn::kHD : attn:
 }  // namespace
 
 long attn_bwd_workspace_floats(int B, int T, int H, int hd) {
-  const long nkb = (T + bwd_kvblk(hd) - 1) / bwd_kvblk(hd);
-  return (nkb * B * H * (long)T * bwd_plane_width(hd) + 1) / 2;  // bf16 planes
+  if (hd == 2 * attn::kHD) {  // bf16 partial planes, one per 128-key block
+    const long nkb = (T + bwd_kvblk(hd) - 1) / bwd_kvblk(hd);
+    return (nkb * B * H * (long)T * bwd_plane_width(hd) + 1) / 2;
+  }
+  // the 8-wave kernel: fp32 dQ accumulator (one [64 rows][64] tile per query tile per (b, h)) or,
+  // split, bf16 partial planes (one per 256-key block)
+  const long ntq = (T + attn::kQTile - 1) / attn::kQTile;
+  const long acc = (long)B * H * ntq * attn::kQTile * attn::kHD;
+  const long nkb = (T + attn::kKvBlk - 1) / attn::kKvBlk;
+  const long planes = (nkb * B * H * (long)T * attn::kHD + 1) / 2;
+  return acc > planes ? acc : planes;
 }
 
 namespace {
@@ -920,10 +984,15 @@ void attn_bwd_probe_set(unsigned long long* buf) {
 
 template <bool DROPOUT, bool KMASK, bool SMALLHD>
 static void launch_bwd_variant(dim3 grid, hipStream_t stream, const bf16_raw* qkv, const bf16_raw* dout,
-                               const float* lse, const float* delta, const bf16_raw* out_o, bf16_raw* dqkv,
-                               float* dq_part, float* vparts, const AttnDims& d, int nkb, DropoutArgs dr) {
-  hipLaunchKernelGGL((attn::attn_bwd_kernel<DROPOUT, KMASK, SMALLHD>), grid, dim3(512), 0, stream, qkv, dout, lse,
-                     delta, out_o, dqkv, dq_part, vparts, d.T, d.H, nkb, dr, d.hd, d.scale, d.key_valid);
+                               const float* lse, const float* delta, bf16_raw* dqkv,
+                               float* dq_acc, float* vparts, float* qparts, const AttnDims& d, int nkb,
+                               DropoutArgs dr) {
+  if (grid.y > 1)
+    hipLaunchKernelGGL((attn::attn_bwd_kernel<DROPOUT, KMASK, SMALLHD, true>), grid, dim3(512), 0, stream, qkv, dout,
+                       lse, delta, dqkv, dq_acc, vparts, qparts, d.T, d.H, nkb, dr, d.hd, d.scale, d.key_valid);
+  else
+    hipLaunchKernelGGL((attn::attn_bwd_kernel<DROPOUT, KMASK, SMALLHD, false>), grid, dim3(512), 0, stream, qkv, dout,
+                       lse, delta, dqkv, dq_acc, vparts, qparts, d.T, d.H, nkb, dr, d.hd, d.scale, d.key_valid);
 }
 
 hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse, void* dqkv,
@@ -939,20 +1008,10 @@ hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, c
   float* vparts = dbias != nullptr ? bias_ws : nullptr;
   float* qparts = dbias != nullptr ? bias_ws + (long)bp.nv * bp.cols : nullptr;
   float* scratch = dbias != nullptr ? bias_ws + (long)(bp.nv + bp.nq) * bp.cols : nullptr;
-  // LLMT_ATTN_FUSED_DELTA=1: the 8-wave kernel forms delta (and, without dropout, the V-bias
-  // column sums) itself while staging each query tile instead of a separate delta pass.  Alone it
-  // is 2% faster at B=128 (1.085 vs 1.110 ms), but in the 124M step -0.4% (1.0555M vs 1.0596M
-  // tok/s, profiles/r2/ab_fused_delta.txt): the longer main kernel overlaps the side stream worse
-  // than the short delta pass, so the default is the separate pass.
-  static const bool fused_delta_env = [] {
-    const char* e = std::getenv("LLMT_ATTN_FUSED_DELTA");
-    return e && std::atoi(e) == 1;
-  }();
-  const bool fuse_delta = !delta_ready && !hd128 && fused_delta_env;
   const bool v_from_delta = !delta_ready && dropout.thr == 0 && dbias != nullptr;
   const dim3 dgrid((T + attn::kDeltaRows - 1) / attn::kDeltaRows, B * H);
   const bool small = hd < attn::kHD;
-  if (!delta_ready && !fuse_delta) {
+  if (!delta_ready) {
     auto dk = hd128 ? attn::attn_delta_kernel<false, 2>
                     : (small ? attn::attn_delta_kernel<true> : attn::attn_delta_kernel<false>);
     hipLaunchKernelGGL(dk, dgrid, dim3(256), 0, stream, (const bf16_raw*)dout, (const bf16_raw*)out, delta,
@@ -960,44 +1019,55 @@ hipError_t launch_attn_bwd(const void* dout, const void* qkv, const void* out, c
   }
   const int kvblk = bwd_kvblk(hd);
   const int nkb = (T + kvblk - 1) / kvblk;
-  const dim3 grid(B * H, nkb);
   const bool drop = dropout.thr != 0, km = d.key_valid != nullptr;
   const int variant = (drop ? 4 : 0) | (km ? 2 : 0) | (small ? 1 : 0);
   auto q = (const bf16_raw*)qkv;
   auto g = (const bf16_raw*)dout;
   auto dq = (bf16_raw*)dqkv;
-  // the main kernel forms the V-bias partials with dropout (per key block) and with the fused delta
-  // (key block 0's column sums of dO, one row per batch)
-  float* vp = (drop || (fuse_delta && v_from_delta)) ? vparts : nullptr;
-  const bf16_raw* out_o = fuse_delta ? (const bf16_raw*)out : nullptr;
+  // the main kernel forms the V-bias partials with dropout (per key block)
+  float* vp = drop ? vparts : nullptr;
+  int nq_rows = bp.nq;  // partial rows of the Q-bias column sums
   if (hd128) {
     auto k = drop ? (km ? attn::attn_bwd128_kernel<true, true> : attn::attn_bwd128_kernel<true, false>)
                   : (km ? attn::attn_bwd128_kernel<false, true> : attn::attn_bwd128_kernel<false, false>);
-    hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, q, g, lse, delta, dq, dq_part, vp, T, H, nkb, dropout,
-                       d.key_valid);
+    hipLaunchKernelGGL(k, dim3(B * H, nkb), dim3(256), 0, stream, q, g, lse, delta, dq, dq_part, vp, T, H, nkb,
+                       dropout, d.key_valid);
+    // dQ: sum of the key blocks' bf16 partial planes (+ the Q-bias partial rows)
+    hipLaunchKernelGGL((attn::attn_dq_reduce_kernel<false, 2>), dim3(B * H, (T + attn::kDqRows - 1) / attn::kDqRows),
+                       dim3(256), 0, stream, (const bf16_raw*)dq_part, dq, qparts, T, H, hd, nkb,
+                       rows * (long)bwd_plane_width(hd), kvblk);
   } else {
+  // one workgroup per (b, h) over its key blocks (fp32 dQ inside, no reduce pass) when B*H fills
+  // the CUs evenly (>= 85 % of the slots of its last round) and there is no dropout (the dropout
+  // body spills in that form); else one per (b, h, key block).  Same box, B = 128 / 32, H = 12
+  // (1,536 / 384 pairs): 0.98 vs 1.11 ms per-(b, h), 0.34 vs 0.31 ms split.
+  const int ncu = device_cu_count(), pairs = B * H;
+  const bool split = nkb > 1 && (drop || (long)pairs * 100 < 85L * ncu * ((pairs + ncu - 1) / ncu));
+  const dim3 grid(pairs, split ? nkb : 1);
   switch (variant) {
-    case 0: launch_bwd_variant<false, false, false>(grid, stream, q, g, lse, delta, out_o, dq, dq_part, vp, d, nkb, dropout); break;
-    case 1: launch_bwd_variant<false, false, true>(grid, stream, q, g, lse, delta, out_o, dq, dq_part, vp, d, nkb, dropout); break;
-    case 2: launch_bwd_variant<false, true, false>(grid, stream, q, g, lse, delta, out_o, dq, dq_part, vp, d, nkb, dropout); break;
-    case 3: launch_bwd_variant<false, true, true>(grid, stream, q, g, lse, delta, out_o, dq, dq_part, vp, d, nkb, dropout); break;
-    case 4: launch_bwd_variant<true, false, false>(grid, stream, q, g, lse, delta, out_o, dq, dq_part, vp, d, nkb, dropout); break;
-    case 5: launch_bwd_variant<true, false, true>(grid, stream, q, g, lse, delta, out_o, dq, dq_part, vp, d, nkb, dropout); break;
-    case 6: launch_bwd_variant<true, true, false>(grid, stream, q, g, lse, delta, out_o, dq, dq_part, vp, d, nkb, dropout); break;
-    default: launch_bwd_variant<true, true, true>(grid, stream, q, g, lse, delta, out_o, dq, dq_part, vp, d, nkb, dropout); break;
+    case 0: launch_bwd_variant<false, false, false>(grid, stream, q, g, lse, delta, dq, dq_part, vp, qparts, d, nkb, dropout); break;
+    case 1: launch_bwd_variant<false, false, true>(grid, stream, q, g, lse, delta, dq, dq_part, vp, qparts, d, nkb, dropout); break;
+    case 2: launch_bwd_variant<false, true, false>(grid, stream, q, g, lse, delta, dq, dq_part, vp, qparts, d, nkb, dropout); break;
+    case 3: launch_bwd_variant<false, true, true>(grid, stream, q, g, lse, delta, dq, dq_part, vp, qparts, d, nkb, dropout); break;
+    case 4: launch_bwd_variant<true, false, false>(grid, stream, q, g, lse, delta, dq, dq_part, vp, qparts, d, nkb, dropout); break;
+    case 5: launch_bwd_variant<true, false, true>(grid, stream, q, g, lse, delta, dq, dq_part, vp, qparts, d, nkb, dropout); break;
+    case 6: launch_bwd_variant<true, true, false>(grid, stream, q, g, lse, delta, dq, dq_part, vp, qparts, d, nkb, dropout); break;
+    default: launch_bwd_variant<true, true, true>(grid, stream, q, g, lse, delta, dq, dq_part, vp, qparts, d, nkb, dropout); break;
   }
+  if (split) {
+    auto rk = small ? attn::attn_dq_reduce_kernel<true> : attn::attn_dq_reduce_kernel<false>;
+    hipLaunchKernelGGL(rk, dim3(pairs, (T + attn::kDqRows - 1) / attn::kDqRows), dim3(256), 0, stream,
+                       (const bf16_raw*)dq_part, dq, qparts, T, H, hd, nkb, rows * (long)attn::kHD, kvblk);
   }
-  const dim3 rgrid(B * H, (T + attn::kDqRows - 1) / attn::kDqRows);
-  auto rk = hd128 ? attn::attn_dq_reduce_kernel<false, 2>
-                  : (small ? attn::attn_dq_reduce_kernel<true> : attn::attn_dq_reduce_kernel<false>);
-  hipLaunchKernelGGL(rk, rgrid, dim3(256), 0, stream, (const bf16_raw*)dq_part, dq, qparts, T, H, hd, nkb,
-                     rows * (long)bwd_plane_width(hd), kvblk);
+  nq_rows = split ? bp.nq : B;
+  }
   if (dbias != nullptr) {
-    // fixed-order sums of the partial rows: Q part, then (unless the out-proj GEMM's epilogue
+    // fixed-order sums of the partial rows: Q part (a row per (b, row tile) from the hd-128 dQ
+    // reduce, a row per b from the 8-wave kernel), then (unless the out-proj GEMM's epilogue
     // already added it) the V part; the K part of the qkv-bias gradient is exactly zero
-    hipError_t e = launch_colsum_reduce(qparts, bp.nq, bp.cols, dbias, scratch, stream);
+    hipError_t e = launch_colsum_reduce(qparts, nq_rows, bp.cols, dbias, scratch, stream);
     if (e != hipSuccess) return e;
-    const int nv = drop ? B * nkb : (v_from_delta ? (fuse_delta ? B : (int)dgrid.x * B) : 0);
+    const int nv = drop ? B * nkb : (v_from_delta ? (int)dgrid.x * B : 0);
     if (nv > 0) {
       e = launch_colsum_reduce(vparts, nv, bp.cols, dbias + 2L * H * hd, scratch, stream);
       if (e != hipSuccess) return e;

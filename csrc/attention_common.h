@@ -17,6 +17,7 @@ typedef short short4v __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) short4v lds_short4;
+typedef __attribute__((address_space(3))) void lds_void;
 
 // Dispatch order of a (B*H) x nblk attention grid (x fastest): (b, h) pairs in chunks of
 // kDispatchChunk; inside a chunk every pair's heaviest block first, then the next-heaviest, ...

@@ -33,6 +33,17 @@ typedef unsigned short ushort4_t __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 
+// compute units of the current device (queried once per process; every MI355X has 256)
+inline int device_cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
 __device__ __forceinline__ float bf2f(bf16_raw v) { return __uint_as_float(((uint32_t)v) << 16); }
 
 __device__ __forceinline__ bf16_raw f2bf(float f) {

@@ -69,15 +69,7 @@ __device__ __forceinline__ int xcd_remap(int L, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
 }
 
-inline int cu_count() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-  }
-  return n;
-}
+inline int cu_count() { return device_cu_count(); }
 
 }  // namespace gemm
 }  // namespace llmt

@@ -66,6 +66,10 @@ CASES = [
     (2, 1024, 8, 128, None),  # head dim 128: two 64-wide halves, the 4-wave backward
     (1, 70, 2, 128, None),
     (3, 300, 4, 128, "mixed"),
+    # B*H filling the CUs evenly: the per-(b, h) workgroup with fp32 dQ accumulation (the smaller
+    # grids above take the per-key-block split with bf16 partial planes + reduce)
+    (32, 300, 8, 48, "mixed"),
+    (20, 1024, 12, 64, "mixed"),
 ]
 
 
@@ -142,14 +146,14 @@ def test_padding_does_not_change_valid_rows(gpu_device) -> None:
     torch.testing.assert_close(out.view(B, T, -1)[:, :L].float(), out_p.view(B, L, -1).float(), atol=0, rtol=0)
 
 
-@pytest.mark.parametrize("hd", [64, 128])
-def test_attention_dropout_head_dims(gpu_device, hd: int) -> None:
-    """Probability dropout at head dims 64 and 128 against the counter-based torch reference
-    (``ops/reference.py``: the same keep mask, the undropped normaliser in lse)."""
+@pytest.mark.parametrize("hd,B,T,H", [(64, 2, 200, 3), (128, 2, 200, 3), (64, 64, 300, 4)])
+def test_attention_dropout_head_dims(gpu_device, hd: int, B: int, T: int, H: int) -> None:
+    """Probability dropout at head dims 64 and 128 (and, B*H = 256, the per-(b, h) backward grid)
+    against the counter-based torch reference (``ops/reference.py``: the same keep mask, the
+    undropped normaliser in lse)."""
     from llmtrain.ops import reference as ref
 
     g = torch.Generator(device="cpu").manual_seed(hd)
-    B, T, H = 2, 200, 3
     qkv = torch.randn(B * T, 3 * hd * H, generator=g).to(torch.bfloat16)
     dout = torch.randn(B * T, hd * H, generator=g).to(torch.bfloat16)
     adrop = (0.25, ref.dropout_site_seed(11, 8))

@@ -89,6 +89,21 @@ __device__ __forceinline__ bf16x8 lds_tr_read_operand(const bf16_raw* tile, int 
   return __builtin_bit_cast(bf16x8, all);
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Join the two 32-lane halves of a wave (the two key halves of a swapped-S^T row): one
+// v_permlane32_swap (gfx950) instead of the ds_bpermute + address arithmetic + lgkmcnt(0) wait that
+// __shfl_xor(x, 32) compiles to.  With x in both operands the swap leaves {x[l], x[l ^ 32]} in every
+// lane l (in some order), so max / sum of the pair is the reduction over both halves.
+__device__ __forceinline__ float halves_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float halves_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // row (within a 32x32 accumulator tile) held in register r by lane half `half`
 __device__ __forceinline__ int acc_row(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 

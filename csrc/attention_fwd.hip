@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, s[kt][r]);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax = halves_max(tmax);
       // lazy rescale: keep a stale running max while no row's max grew by more than 2^8 in
       // probability (P <= 256 is exact enough in fp32 and bf16; l and O use the same stale max,
       // so the result is unchanged).  The O/l rescale (16 packed muls + one exp per lane) then
@@ -224,17 +224,24 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
       }
       // an all-masked row so far (KMASK only) has m = -inf: offset 0 gives P = 0, not NaN
       const float mc = (KMASK && m_run == -INFINITY) ? 0.f : m_run * c;
-      float psum = 0.f;
+      // exponent arguments and the row sum in packed fp32 (v_pk_fma_f32 / v_pk_add_f32: half the
+      // VALU issue of the scalar forms; the loop is VALU-issue bound).  The sum stays per lane half
+      // (this lane's 32 keys of the tile): l_run is joined across the halves once, after the sweep.
+      const f32x2 cc = {c, c}, nmc = {-mc, -mc};
+      f32x2 ps = {0.f, 0.f};
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], c, -mc));  // v_exp_f32, no denorm fixup
-          s[kt][r] = p;
-          psum += p;
+        for (int r = 0; r < 16; r += 2) {
+          const f32x2 x = {s[kt][r], s[kt][r + 1]};
+          const f32x2 y = __builtin_elementwise_fma(x, cc, nmc);
+          const f32x2 p = {__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};  // v_exp_f32
+          s[kt][r] = p[0];
+          s[kt][r + 1] = p[1];
+          ps += p;
         }
       }
-      psum += __shfl_xor(psum, 32, 64);
+      const float psum = ps[0] + ps[1];
       if (DROPOUT) {  // the normaliser sums the undropped P; P V uses the masked, rescaled P
         const uint32_t e_q = (uint32_t)q * (uint32_t)T + (uint32_t)(kbase + 4 * half);
 #pragma unroll
@@ -271,6 +278,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
     if (it + 1 < ntiles) tile_step(it + 1, st0);
   }
 
+  l_run = halves_sum(l_run);  // both key halves of the row (every rescale hit both alike)
   if (q < T) {
     // a row that never saw an unpadded key: O = 0 and lse = +inf (P = 0 in the backward)
     const bool dead = KMASK && m_run == -INFINITY;

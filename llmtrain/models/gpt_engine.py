@@ -228,8 +228,8 @@ class FusedGPTEngine:
             with torch.cuda.stream(side):
                 ops.wgrad_accum(dst, dy, x)
             self._pending.extend((dy, x))
-        else:
-            ops.wgrad_accum(dst, dy, x)
+        else:  # one stream: nothing runs beside it, so the 512-register pipelined kernel
+            ops.wgrad_accum(dst, dy, x, exclusive=True)
 
     def _retire_block(self) -> None:
         """End of one block's backward: fence its side-stream GEMMs with an event and release the

@@ -45,6 +45,7 @@ for step in "$@"; do
         python3 bench.py --gpus 1 --steps 6 --warmup 3 --micro-batch "$mb"
       db=$(find "$d" -name "*.db" | head -1)
       python3 scripts/rocpd_stats.py "$db" 3 40 > "$OUT/kernel_stats_mb$mb.txt" 2>&1 || true
+      python3 scripts/rocpd_timeline.py "$db" 3 > "$OUT/timeline_mb$mb.txt" 2>&1 || true
       rm -f "$db"
       cat "$OUT/kernel_stats_mb$mb.txt" ;;
     det)

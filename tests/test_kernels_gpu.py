@@ -233,7 +233,8 @@ def test_wgrad_gemm(gpu_device, M, N, K, lda, tile):
 
 
 # ---- fused forward / dX GEMM (csrc/gemm_fused.hip) -------------------------------------------
-GEMM_SHAPES = [(4096, 3072, 768), (8192, 3072, 768), (513, 768, 3072), (1000, 200, 256), (300, 2304, 768)]
+GEMM_SHAPES = [(4096, 3072, 768), (8192, 3072, 768), (513, 768, 3072), (1000, 200, 256), (300, 2304, 768),
+               (65536 + 96, 768, 256)]  # >= kWideM m-tiles: one raster band over all of N, ragged M
 
 
 def _gemm_operands(M, N, K, b_kn, dev, seed):

@@ -9,10 +9,12 @@
 //  * and cheaper than contended atomics: the delta / dQ-reduce passes of the attention backward
 //    sent 512-2048 atomic adds to each bias address (MI355X_MICROARCH: same-address atomics
 //    serialise at the memory side).
-// Workgroup = 64 columns (one per lane: coalesced 256-byte rows) x 4 waves, each wave summing a
-// contiguous quarter of the parts in order, the quarters added in wave order.  Up to 256 parts:
+// Workgroup = 64 columns (one per lane: coalesced 256-byte rows) x 8 waves, each wave summing a
+// contiguous eighth of the parts in order, the eighths added in wave order.  Up to 256 parts:
 // one pass into dst; above: groups of 128 parts -> scratch[g][c], then the groups -> dst (two
-// launches, 4 dependent load rounds each).  Several same-shape reductions share one launch
+// launches).  The launches are latency-bound (12-48 workgroups, one per 64 columns), so a lane
+// issues all of a round's 16 loads before the first add: <= 2 dependent load rounds per launch
+// (was 8 with 4 waves x 8 loads: ~9 us per reduce, ~100 reduces per step).  Several same-shape reductions share one launch
 // (launch_colsum_reduce_multi: LayerNorm backward's 2-3 column sums).
 //
 // embedding_bwd_sorted_kernel: dwte[v] += sum of dx rows whose token is v, over the rows in
@@ -26,9 +28,10 @@ namespace llmt {
 namespace {
 
 constexpr int kStrip = 64;      // columns per workgroup: one per lane, 256-byte coalesced rows
-constexpr int kWaves = 4;       // waves per workgroup, each summing a contiguous quarter of the parts
+constexpr int kWaves = 8;       // waves per workgroup, each summing a contiguous eighth of the parts
 constexpr int kOneLevel = 256;  // up to this many parts: one pass straight into dst
-constexpr int kGroup = 128;     // parts per first-level group above that (32 per wave)
+constexpr int kGroup = 128;     // parts per first-level group above that (16 per wave)
+constexpr int kInFlight = 16;   // loads a lane issues before it adds
 
 // One job = one (parts, dst, scratch) triple; up to kMaxJobs jobs of the same shape share a
 // launch (blockIdx.z), e.g. LayerNorm backward's dgamma / dbeta / projection-bias rows.
@@ -38,12 +41,12 @@ struct Jobs {
   float* dst[kMaxJobs];
 };
 
-// out[g][c] (+)= sum_{p in group g} parts[p][c].  Wave w of the workgroup sums its quarter of the
-// group's parts in order (8 loads in flight per lane), the quarters are added in wave order
+// out[g][c] (+)= sum_{p in group g} parts[p][c].  Wave w of the workgroup sums its eighth of the
+// group's parts in order (kInFlight loads in flight per lane), the eighths are added in wave order
 // through LDS: a fixed association for a given (nparts, group), hence bitwise reproducible.
 // `accumulate` (final level) adds into column c of a [rows][row_len] view with leading dimension
 // out_ld; otherwise the group's sum is stored to out[g][c].
-__global__ __launch_bounds__(256) void colsum_parts_kernel(Jobs jobs, int nparts, int group, long ncols,
+__global__ __launch_bounds__(64 * kWaves) void colsum_parts_kernel(Jobs jobs, int nparts, int group, long ncols,
                                                            int row_len, long out_ld, bool accumulate) {
   __shared__ float red[kWaves][kStrip];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -56,19 +59,27 @@ __global__ __launch_bounds__(256) void colsum_parts_kernel(Jobs jobs, int nparts
   float acc = 0.f;
   if (c < ncols) {
     int p = w0;
-    for (; p + 8 <= w1; p += 8) {
-      float v[8];
+    for (; p + kInFlight <= w1; p += kInFlight) {
+      float v[kInFlight];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = parts[(long)(p + i) * ncols + c];
+      for (int i = 0; i < kInFlight; ++i) v[i] = parts[(long)(p + i) * ncols + c];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc += v[i];
+      for (int i = 0; i < kInFlight; ++i) acc += v[i];
     }
-    for (; p < w1; ++p) acc += parts[(long)p * ncols + c];
+    if (p < w1) {  // the remainder as one more round (adding 0.f past w1 leaves acc unchanged)
+      float v[kInFlight];
+#pragma unroll
+      for (int i = 0; i < kInFlight; ++i) v[i] = p + i < w1 ? parts[(long)(p + i) * ncols + c] : 0.f;
+#pragma unroll
+      for (int i = 0; i < kInFlight; ++i) acc += v[i];
+    }
   }
   red[wave][lane] = acc;
   __syncthreads();
   if (wave != 0 || c >= ncols) return;
-  const float sum = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  float sum = red[0][lane];
+#pragma unroll
+  for (int w = 1; w < kWaves; ++w) sum += red[w][lane];
   float* out = jobs.dst[blockIdx.z];
   if (accumulate) {
     out[(c / row_len) * out_ld + c % row_len] += sum;
@@ -135,7 +146,7 @@ hipError_t launch_colsum_reduce_multi(const float* const* parts, float* const* d
     row_len = (int)ncols;
     dst_ld = ncols;
   }
-  const dim3 block(256);
+  const dim3 block(64 * kWaves);
   const unsigned gx = (unsigned)((ncols + kStrip - 1) / kStrip);
   Jobs final_jobs{}, first{};
   const int groups = num_groups(nparts);

@@ -9,12 +9,15 @@
 //  * and cheaper than contended atomics: the delta / dQ-reduce passes of the attention backward
 //    sent 512-2048 atomic adds to each bias address (MI355X_MICROARCH: same-address atomics
 //    serialise at the memory side).
-// Workgroup = 64 columns (one per lane: coalesced 256-byte rows) x 8 waves, each wave summing a
-// contiguous eighth of the parts in order, the eighths added in wave order.  Up to 256 parts:
-// one pass into dst; above: groups of 128 parts -> scratch[g][c], then the groups -> dst (two
-// launches).  The launches are latency-bound (12-48 workgroups, one per 64 columns), so a lane
-// issues all of a round's 16 loads before the first add: <= 2 dependent load rounds per launch
-// (was 8 with 4 waves x 8 loads: ~9 us per reduce, ~100 reduces per step).  Several same-shape reductions share one launch
+// Workgroup = 64 columns (one per lane: coalesced 256-byte rows) x 16 waves, each wave summing a
+// contiguous sixteenth of the parts in order, the sixteenths added in wave order.  Up to 2048
+// parts: one pass into dst; above: groups of 128 parts -> scratch[g][c], then the groups -> dst
+// (two launches).  The launches are latency-bound (12-48 workgroups, one per 64 columns) and a
+// launch costs ~4 us by itself, so a lane issues a whole round of 16 loads before the first add
+// and the one-pass range covers every reduce of the GPT-2 124M step (LayerNorm backward's ~1,024
+// partial rows, the GEMM epilogues' M / 128, the attention's per-row-tile rows): <= 4 dependent
+// load rounds in ONE launch (was 4 waves x 8 loads: two launches of up to 8 rounds above 256
+// parts; 9.4 us per reduce at micro-batch 32, ~100 reduces per step).  Several same-shape reductions share one launch
 // (launch_colsum_reduce_multi: LayerNorm backward's 2-3 column sums).
 //
 // embedding_bwd_sorted_kernel: dwte[v] += sum of dx rows whose token is v, over the rows in
@@ -28,9 +31,9 @@ namespace llmt {
 namespace {
 
 constexpr int kStrip = 64;      // columns per workgroup: one per lane, 256-byte coalesced rows
-constexpr int kWaves = 8;       // waves per workgroup, each summing a contiguous eighth of the parts
-constexpr int kOneLevel = 256;  // up to this many parts: one pass straight into dst
-constexpr int kGroup = 128;     // parts per first-level group above that (16 per wave)
+constexpr int kWaves = 16;      // waves per workgroup, each summing a contiguous sixteenth of the parts
+constexpr int kOneLevel = 2048; // up to this many parts: one pass straight into dst
+constexpr int kGroup = 128;     // parts per first-level group above that (8 per wave)
 constexpr int kInFlight = 16;   // loads a lane issues before it adds
 
 // One job = one (parts, dst, scratch) triple; up to kMaxJobs jobs of the same shape share a
@@ -41,8 +44,8 @@ struct Jobs {
   float* dst[kMaxJobs];
 };
 
-// out[g][c] (+)= sum_{p in group g} parts[p][c].  Wave w of the workgroup sums its eighth of the
-// group's parts in order (kInFlight loads in flight per lane), the eighths are added in wave order
+// out[g][c] (+)= sum_{p in group g} parts[p][c].  Wave w of the workgroup sums its sixteenth of
+// the group's parts in order (kInFlight loads in flight per lane), they are added in wave order
 // through LDS: a fixed association for a given (nparts, group), hence bitwise reproducible.
 // `accumulate` (final level) adds into column c of a [rows][row_len] view with leading dimension
 // out_ld; otherwise the group's sum is stored to out[g][c].

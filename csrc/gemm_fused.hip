@@ -211,6 +211,13 @@ struct Args {
   int M, N, K;
   int tiles_m, tiles_n, ntiles, nwg;
   int band;  // n-tiles per raster band (tile_origin)
+  // non-temporal epilogue I/O (C / C2 stores, U loads): from kWideM m-tiles on the 0.2-1.6 GB of
+  // output streams past every cache and, left temporal, evicts the weight and the activation strip
+  // the tile order keeps in L2 / the Infinity Cache.  M = 131072: qkv fwd 0.517 -> 0.419 ms, fc fwd
+  // 0.630 -> 0.533, fc fwd + GELU 0.851 -> 0.725, proj dX 0.622 -> 0.539, dX + dGELU 0.829 ->
+  // 0.771; at M = 32768 mixed (qkv fwd 0.120 -> 0.133), so the rule is tied to the tile order's
+  // (profiles/r3/nt/)
+  int nt;
   int debug;
 };
 
@@ -321,6 +328,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
   const __amdgpu_buffer_rsrc_t rdel = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(EPI == 3 ? p.delta : (float*)p.C), (short)0, EPI == 3 ? p.M * (p.N / 64) * 4 : 0, 0x00020000);
 
+  // output stores / U loads with the non-temporal hint at large M (see Args::nt)
+  auto st16 = [&](u32x4 v, __amdgpu_buffer_rsrc_t rs, int off) {
+    if (p.nt) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 2);
+    else __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
+  };
+
   // Software pipeline over the stage stream (2-slot ring of 64-deep stages; stage g+1 lands while
   // stage g computes).  Iteration g runs its four k16 MFMA groups with every fragment read issued
   // one group ahead; before the last group: wait stage g+1 + retire reads + barrier, DMA stage g+2
@@ -418,7 +431,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
       for (int it = 0; it < 2; ++it) {
         const int m = mw + 16 * mf + 8 * it + (lane >> 3);
         const int uoff = (m < p.M && n < p.N) ? (m * p.ldu + n) * 2 : kOob;
-        dst[it] = __builtin_amdgcn_raw_buffer_load_b128(ru, uoff, 0, 0);
+        dst[it] = p.nt ? __builtin_amdgcn_raw_buffer_load_b128(ru, uoff, 0, 2)
+                        : __builtin_amdgcn_raw_buffer_load_b128(ru, uoff, 0, 0);
       }
     };
     if (EPI >= 2) load_u(0, uraw[0]);
@@ -463,7 +477,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
             dot = fmaf(o[k], bf2f(ov[k]), dot);
             csum[k] += o[k];
           }
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(o)), rc, off[it], 0, 0);
+          st16(__builtin_bit_cast(u32x4, pack8(o)), rc, off[it]);
           // the 8 lanes of one row segment (lane & 7) hold the head's 64 columns
           dot += __shfl_xor(dot, 1, 64);
           dot += __shfl_xor(dot, 2, 64);
@@ -490,7 +504,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
             o[k] = bf2f(f2bf(vals[it][k] * gelu_grad(bf2f(uv[k]))));
             csum[k] += o[k];
           }
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(o)), rc, off[it], 0, 0);
+          st16(__builtin_bit_cast(u32x4, pack8(o)), rc, off[it]);
           // pin the running sums here: left alone, hipcc sinks the adds to the end of the epilogue
           // and keeps every product live (spills)
           asm volatile("" : "+v"(csum[0]), "+v"(csum[1]), "+v"(csum[2]), "+v"(csum[3]), "+v"(csum[4]),
@@ -503,11 +517,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) o[k] = vals[it][k] + bias_f[k];
           const ushort8_t ov = pack8(o);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ov), rc, off[it], 0, 0);
+          st16(__builtin_bit_cast(u32x4, ov), rc, off[it]);
           if (EPI == 1) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) o[k] = gelu(bf2f(ov[k]));
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(o)), rc2, off[it], 0, 0);
+            st16(__builtin_bit_cast(u32x4, pack8(o)), rc2, off[it]);
           }
         }
       }
@@ -586,6 +600,7 @@ hipError_t launch_gemm_fused(const GemmFusedArgs& g, hipStream_t stream) {
   a.debug = dbg ? std::atoi(dbg) : 0;
   // at large M one band spans all of N: see tile_origin
   a.band = a.tiles_m >= kWideM || kBand >= a.tiles_n ? a.tiles_n : kBand;
+  a.nt = a.tiles_m >= kWideM ? 1 : 0;
   switch (g.epilogue * 2 + (g.b_kn ? 1 : 0)) {
     case 0: launch_one<false, 0>(a, stream); break;
     case 1: launch_one<true, 0>(a, stream); break;

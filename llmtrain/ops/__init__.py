@@ -206,7 +206,10 @@ FGEMM_MAX_A_BYTES = 64 * 2**20
 # column sums in the epilogue (deletes the delta pass; same-box mb 128: 1,076.3k vs 1,074.5k tok/s,
 # profiles/r3/ab_dx_attn_any_size_mb128.txt).  Adding the plain dX GEMMs (-0.4 %) or the forward
 # GEMMs (-1.6 %) at this size loses: hipBLASLt's 256x256 kernels run 1.1-1.3 PF on these shapes
-# against 0.86-1.14 PF for ours (profiles/r3/fgemm_wide_v2_ab_m131k.log).
+# against 0.86-1.14 PF for ours (profiles/r3/fgemm_wide_v2_ab_m131k.log).  With non-temporal output
+# stores at this size, fc + bias + GELU on ours beats hipBLASLt + the GELU pass alone (0.725 vs
+# 0.808 ms) but runs 0.86 ms per call inside the step and the step loses 0.4-1.0 % (qkv forward
+# too: -1.2 %; profiles/r3/nt/), so those stay on hipBLASLt.
 FGEMM_ANY_SIZE = frozenset({"dx_gelu", "dx_attn"})
 
 

@@ -76,7 +76,10 @@ __global__ __launch_bounds__(256) void gelu_fwd_tiled_kernel(const void* __restr
 #pragma unroll
   for (int k = 0; k < kU; ++k) {
     const long i = base + k * 256;
-    ld8<BF16>(u, i < n8 ? i : 0, f[k]);  // unconditional: a load under a divergent if waits alone
+    // unconditional: a load under a divergent if waits alone.  Non-temporal: u is next read in the
+    // backward, while g is read by the next GEMM and should keep the cache
+    if (BF16) unpack8(__builtin_nontemporal_load(reinterpret_cast<const ushort8_t*>(u) + (i < n8 ? i : 0)), f[k]);
+    else ld8<BF16>(u, i < n8 ? i : 0, f[k]);
   }
 #pragma unroll
   for (int k = 0; k < kU; ++k)

@@ -6,6 +6,7 @@ GPURUN ?= /usr/local/graft/bin/gpurun
 .PHONY: build test test-gpu bench bench-module profile parity train-smoke train-ddp train-gpt2 train-gpt2-ddp8 \
         generate mlflow format k8s-build k8s-train k8s-logs k8s-clean k8s-e2e k8s-e2e-cpu k8s-train-resilient lint \
         k8s-kind-cluster k8s-kind-delete k8s-kind-smoke k8s-mlflow \
+        k8s-cluster k8s-cluster-delete k8s-full k8s-kind-load train-gpt-ddp \
         k8s-dashboard k8s-dashboard-token k8s-dashboard-proxy k8s-dashboard-delete
 
 build:                 ## compile every HIP kernel for gfx950 into llmtrain/ops/_llmtrain_hip.so
@@ -48,6 +49,9 @@ train-smoke:
 train-ddp:             ## reference DDP smoke: 2 CPU ranks over gloo
 	$(PY) -m torch.distributed.run --nproc_per_node=2 --master-addr 127.0.0.1 -m llmtrain train --config configs/presets/ddp_smoke.yaml
 
+train-gpt-ddp:         ## reference target name: 2 CPU ranks over gloo on the wikitext DDP preset
+	$(PY) -m torch.distributed.run --nproc_per_node=2 --master-addr 127.0.0.1 -m llmtrain train --config configs/presets/gpt_wikitext_ddp.yaml
+
 train-gpt2: build
 	$(PY) -m llmtrain train --config configs/presets/gpt2_124m_mi355x.yaml
 
@@ -86,6 +90,16 @@ k8s-kind-cluster:
 
 k8s-kind-delete:
 	kind delete cluster --name llmtrain
+
+# reference target names (Makefile:30-51 of the reference): kind cluster, then the GPU Job
+k8s-cluster: k8s-kind-cluster
+
+k8s-cluster-delete: k8s-kind-delete
+
+k8s-kind-load: k8s-build
+	kind load docker-image llmtrain-mi355x:dev --name llmtrain
+
+k8s-full: k8s-cluster k8s-kind-load k8s-train k8s-logs
 
 k8s-kind-smoke: k8s-build
 	kind load docker-image llmtrain-mi355x:dev --name llmtrain

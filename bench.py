@@ -277,8 +277,17 @@ def main() -> int:
                                          for k, v in probe.as_dict().items()}
             for b in buckets:  # what the bucket would take alone at the probed bus bandwidth
                 b["alone_ms"] = round(b["payload_mib"] * 2**20 * 2 * (world - 1) / world / probe.busbw_gbps / 1e6, 3)
+        if world > 1:  # the first multi-GPU run has to explain itself (channels, transports)
+            from llmtrain.parallel.comm import rccl_report
+
+            result["rccl"] = rccl_report()
         if buckets:
             result["buckets_rank0"] = buckets
+            # the last bucket (the tied embedding, final in the backward) cannot overlap compute:
+            # its queue + collective time is what the step exposes
+            tail = buckets[-1]
+            result["tail_bucket"] = {k: tail[k] for k in ("bucket", "payload_mib", "queue_ms", "comm_ms", "alone_ms")
+                                     if k in tail}
         print(json.dumps(result), flush=True)
     if ddp_state is not None:
         teardown_ddp()

@@ -10,6 +10,7 @@
 
 #include <torch/library.h>
 
+#include <algorithm>
 #include <cmath>
 
 #include "kernels.h"
@@ -462,6 +463,12 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tens
   TORCH_CHECK((b_kn ? b.size(0) : b.size(1)) == K, "gemm_fused: inner dimensions differ");
   TORCH_CHECK(K % 64 == 0 && K >= 256 && N % 8 == 0, "gemm_fused: needs K % 64 == 0, K >= 256, N % 8 == 0");
   TORCH_CHECK(epilogue >= 0 && epilogue <= 3, "gemm_fused: epilogue must be 0, 1, 2 or 3");
+  // the kernel's buffer descriptors and tile offsets are 32-bit byte offsets: every operand and
+  // output (a [M,K], b, out / u / c2 [M,N]) must stay below 2 GiB, else loads read zeros and
+  // stores drop silently — callers split larger GEMMs into row chunks (llmtrain/ops, _gemm_rows)
+  TORCH_CHECK(M * std::max(K, N) * 2 < (int64_t(1) << 31) && K * N * 2 < (int64_t(1) << 31),
+              "gemm_fused: an operand or output reaches 2 GiB (M=", M, ", K=", K, ", N=", N,
+              "); split the rows");
   // 16-byte LDS-DMA / vector stores on every operand, 4-byte DMA of the bias
   TORCH_CHECK((uintptr_t)a.data_ptr() % 16 == 0 && (uintptr_t)b.data_ptr() % 16 == 0,
               "gemm_fused: operands must be 16-byte aligned");

@@ -16,10 +16,13 @@ carries exactly one JSON document.
 from __future__ import annotations
 
 import argparse
+import io
 import json
 import logging
+import os
 import sys
-from collections.abc import Sequence
+from collections.abc import Callable, Iterator, Sequence
+from contextlib import contextmanager
 from pathlib import Path
 from typing import Any, TextIO
 
@@ -122,6 +125,41 @@ def _route_to_stderr(name: str, template: logging.Logger) -> logging.Logger:
     return child
 
 
+@contextmanager
+def _stdout_reserved(enabled: bool) -> Iterator[Callable[[str], None]]:
+    """In ``--json`` mode give the run's fd 1 to stderr and yield a writer for the real stdout.
+
+    Native libraries write to fd 1 behind Python's back — under ``torchrun`` libgloo prints
+    ``[Gloo] Rank r is connected to ...`` from every rank, RCCL may print its banner — so routing
+    the loggers to stderr is not enough to keep stdout one JSON document (reference contract:
+    cli.py:281-288, 315-322; tests/test_distributed.py:733-761).  fd 1 is pointed at fd 2 before
+    the process group exists and restored afterwards; only the summary goes to the saved fd."""
+    if not enabled:
+        yield lambda text: print(text)
+        return
+    sys.stdout.flush()
+    try:
+        fd = sys.stdout.fileno()
+    except (AttributeError, OSError, io.UnsupportedOperation):
+        # stdout is a Python object (in-process capture): no native writer can reach it
+        yield lambda text: print(text)
+        return
+    saved = os.dup(fd)
+    os.dup2(sys.stderr.fileno(), fd)
+
+    def write(text: str) -> None:
+        data = (text + "\n").encode()
+        while data:
+            data = data[os.write(saved, data):]
+
+    try:
+        yield write
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, fd)
+        os.close(saved)
+
+
 def build_parser() -> argparse.ArgumentParser:
     parser = argparse.ArgumentParser(
         prog="llmtrain",
@@ -192,7 +230,13 @@ def _handle_train(args: argparse.Namespace) -> int:
     except ConfigLoadError as exc:
         _emit_config_error(exc, json_output=args.json)
         return 2
+    with _stdout_reserved(bool(args.json)) as emit:
+        return _train(args, config, raw_path, resolved_path, emit)
 
+
+def _train(
+    args: argparse.Namespace, config: RunConfig, raw_path: str, resolved_path: Any, emit: Callable[[str], None]
+) -> int:
     ddp_state: DDPState | None = setup_ddp(config) if config.ddp.enabled else None
     is_main = ddp_state is None or ddp_state.is_main
     root = config.output.root_dir
@@ -264,7 +308,7 @@ def _handle_train(args: argparse.Namespace) -> int:
             )
         if is_main:
             _log_run_artifacts(tracker, run_dir)
-            print(json.dumps(summary, indent=2) if args.json else summary)
+            emit(json.dumps(summary, indent=2) if args.json else summary)
     finally:
         tracker.end_run()
         if ddp_state is not None:

@@ -16,9 +16,11 @@ from torch.utils.data.distributed import DistributedSampler
 from llmtrain.config.schemas import RunConfig
 
 
-def world_and_rank(cfg: RunConfig) -> tuple[int, int, bool]:
-    if dist.is_available() and dist.is_initialized():
-        world, rank = dist.get_world_size(), dist.get_rank()
+def world_and_rank(cfg: RunConfig, dist_api: Any = dist) -> tuple[int, int, bool]:
+    """``dist_api`` is the ``torch.distributed`` module as the calling data module sees it (each
+    module imports it as ``dist`` and passes it, so tests can patch one module's view)."""
+    if dist_api.is_available() and dist_api.is_initialized():
+        world, rank = dist_api.get_world_size(), dist_api.get_rank()
         return world, rank, world > 1
     world = cfg.ddp.world_size or 1
     rank = cfg.ddp.rank or 0
@@ -33,8 +35,9 @@ def make_loader(
     num_workers: int,
     collate_fn: Any = None,
     pin_memory: bool = False,
+    dist_api: Any = dist,
 ) -> DataLoader:
-    world, rank, sharded = world_and_rank(cfg)
+    world, rank, sharded = world_and_rank(cfg, dist_api)
     shuffle = train and not cfg.run.deterministic
     sampler = None
     if sharded:

@@ -11,6 +11,7 @@ from __future__ import annotations
 from typing import Any
 
 import torch
+import torch.distributed as dist
 from torch.utils.data import DataLoader, Dataset
 
 from llmtrain.config.schemas import RunConfig
@@ -57,11 +58,11 @@ class DummyTextDataModule(DataModule):
     def train_dataloader(self) -> DataLoader:
         if self._cfg is None or self._train is None:
             raise RuntimeError("setup must be called before train_dataloader")
-        return make_loader(self._train, self._cfg, train=True, num_workers=0)
+        return make_loader(self._train, self._cfg, train=True, num_workers=0, dist_api=dist)
 
     def val_dataloader(self) -> DataLoader | None:
         if self._cfg is None:
             raise RuntimeError("setup must be called before val_dataloader")
         if self._val is None:
             return None
-        return make_loader(self._val, self._cfg, train=False, num_workers=0)
+        return make_loader(self._val, self._cfg, train=False, num_workers=0, dist_api=dist)

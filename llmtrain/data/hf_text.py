@@ -13,6 +13,7 @@ from pathlib import Path
 from typing import Any
 
 import torch
+import torch.distributed as dist
 from torch.utils.data import DataLoader
 
 from llmtrain.config.schemas import RunConfig
@@ -113,7 +114,8 @@ class HFTextDataModule(DataModule):
         if self._cfg is None or self._train_dataset is None:
             raise RuntimeError("setup must be called before train_dataloader")
         return make_loader(
-            self._train_dataset, self._cfg, train=True, num_workers=self._cfg.data.num_workers, collate_fn=_collate
+            self._train_dataset, self._cfg, train=True, num_workers=self._cfg.data.num_workers, collate_fn=_collate,
+            dist_api=dist,
         )
 
     def val_dataloader(self) -> DataLoader | None:
@@ -122,5 +124,6 @@ class HFTextDataModule(DataModule):
         if self._val_dataset is None:
             return None
         return make_loader(
-            self._val_dataset, self._cfg, train=False, num_workers=self._cfg.data.num_workers, collate_fn=_collate
+            self._val_dataset, self._cfg, train=False, num_workers=self._cfg.data.num_workers, collate_fn=_collate,
+            dist_api=dist,
         )

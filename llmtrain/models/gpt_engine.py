@@ -251,7 +251,7 @@ class FusedGPTEngine:
             torch.cuda.current_stream().wait_event(old)
 
     def _side_stream(self) -> torch.cuda.Stream | None:
-        if not self.wgrad_stream_enabled or not self.store.device.type == "cuda":
+        if not self.wgrad_stream_enabled or not self.store.device.type == "cuda" or ops.single_stream():
             return None
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.store.device)
@@ -273,6 +273,8 @@ class FusedGPTEngine:
         return torch.mm(x, w.t()) if b is None else torch.addmm(b, x, w.t())
 
     def loss(self, ids: torch.Tensor, labels: torch.Tensor, mask: torch.Tensor | None) -> torch.Tensor:
+        if not self.fused_gemm and self.store.device.type == "cuda":
+            ops._det_fallback("every GEMM (LLMTRAIN_FUSED_GEMM=0)")
         self.store.sync_shadow()
         if torch.is_grad_enabled():
             return _FusedLoss.apply(self._anchor, self, ids, labels, mask)

@@ -35,6 +35,7 @@ __all__ = [
     "linear_fwd_gelu",
     "scale",
     "set_deterministic",
+    "single_stream",
     "sumsq",
 ]
 
@@ -48,23 +49,43 @@ def _on_gpu(t: torch.Tensor) -> bool:
     return t.device.type == "cuda"
 
 
-_POLICY = {"gemm_all_ours": False}
+_POLICY = {"gemm_all_ours": False, "single_stream": False}
+
+# How run.deterministic keeps the step bitwise reproducible (LLMTRAIN_DET_SCHEDULE overrides):
+#  * "serial": the weight-gradient GEMMs run on the main stream (no side stream), the forward / dX
+#    GEMMs stay on hipBLASLt's tuned solutions.  Nothing runs beside a library GEMM, so the timing
+#    perturbation that made hipBLASLt's Stream-K solutions diverge (docs/round3.md section 2) is
+#    gone; costs the overlap of the two streams (~1 %).
+#  * "ours": every forward / dX GEMM on the hand-written kernel (csrc/gemm_fused.hip), side stream
+#    kept; slower because that kernel trails hipBLASLt at 128K rows (docs/round4.md).
+DET_SCHEDULES = ("serial", "ours")
 
 
-def set_deterministic(on: bool) -> bool:
+def set_deterministic(on: bool, schedule: str | None = None) -> bool:
     """Process-wide deterministic mode of the HIP kernels (``run.deterministic`` on GPU): the
     split-K weight-gradient GEMM and the embedding token gradient switch from float atomics to
-    fixed-order reductions (every other reduction is fixed-order always), and EVERY forward / dX
-    GEMM runs on the hand-written kernel (csrc/gemm_fused.hip) — hipBLASLt's Stream-K solutions
-    combine partial tiles in an order that depends on which workgroups finish first, which the
-    weight-gradient side stream perturbs (bench/determinism_probe.py --runs, docs/round3.md).
-    Returns the previous setting.  The CPU reference ops are deterministic anyway."""
-    _POLICY["gemm_all_ours"] = bool(on)
+    fixed-order reductions (every other reduction is fixed-order always), and the GEMM schedule
+    becomes one of :data:`DET_SCHEDULES` — hipBLASLt's Stream-K solutions combine partial tiles in
+    an order that depends on which workgroups finish first, which the weight-gradient side stream
+    perturbs (bench/determinism_probe.py --runs, docs/round3.md).  Returns the previous setting.
+    The CPU reference ops are deterministic anyway."""
+    import os
+
+    schedule = schedule or os.environ.get("LLMTRAIN_DET_SCHEDULE", "serial")
+    if schedule not in DET_SCHEDULES:
+        raise ValueError(f"deterministic schedule must be one of {DET_SCHEDULES}, not {schedule!r}")
+    _POLICY["gemm_all_ours"] = bool(on) and schedule == "ours"
+    _POLICY["single_stream"] = bool(on) and schedule == "serial"
     if not _ext.load():
         return False
     prev = bool(torch.ops.llmtrain_hip.get_deterministic())
     torch.ops.llmtrain_hip.set_deterministic(bool(on))
     return prev
+
+
+def single_stream() -> bool:
+    """True when the deterministic "serial" schedule forbids the weight-gradient side stream."""
+    return _POLICY["single_stream"]
 
 
 def add_layernorm_fwd(x, delta, weight, bias, eps: float, out_dtype: torch.dtype, dropout=(0.0, 0)):
@@ -213,21 +234,69 @@ FGEMM_MAX_A_BYTES = 64 * 2**20
 FGEMM_ANY_SIZE = frozenset({"dx_gelu", "dx_attn"})
 
 
+_WARNED: set[str] = set()
+
+
+def _det_fallback(what: str) -> None:
+    """Deterministic mode promises every forward / dX GEMM on the hand-written kernel; a shape it
+    cannot take runs on hipBLASLt, whose Stream-K solutions are not run-to-run reproducible beside
+    the weight-gradient side stream.  Say so once per distinct case instead of failing silently."""
+    if _POLICY["gemm_all_ours"] and what not in _WARNED:
+        _WARNED.add(what)
+        import warnings
+
+        warnings.warn(
+            f"run.deterministic: {what} runs on hipBLASLt (not bitwise reproducible run to run); "
+            "set LLMTRAIN_WGRAD_STREAM=0 for a reproducible schedule", RuntimeWarning, stacklevel=3,
+        )
+
+
 def _fgemm_ok(a: torch.Tensor, k: int, n: int, *others: torch.Tensor | None, op: str = "") -> bool:
     """Shapes/placements the fused MFMA GEMM (csrc/gemm_fused.hip) takes and wins on:
     K % 64 == 0, K >= 256, N % 8 == 0, 16-byte aligned operands, A small enough (see above)."""
     if not (k % 64 == 0 and k >= 256 and n % 8 == 0):
+        _det_fallback(f"GEMM {op or 'linear'} K={k} N={n} (needs K % 64 == 0, K >= 256, N % 8 == 0)")
         return False
     if a.numel() * a.element_size() > FGEMM_MAX_A_BYTES and op not in FGEMM_ANY_SIZE and not _POLICY["gemm_all_ours"]:
         return False
-    return all(t is None or t.data_ptr() % 16 == 0 for t in (a, *others))
+    if not all(t is None or t.data_ptr() % 16 == 0 for t in (a, *others)):
+        _det_fallback(f"GEMM {op or 'linear'} with an operand not 16-byte aligned")
+        return False
+    return True
+
+
+# The hand-written GEMM's buffer descriptors and tile offsets are 32-bit byte offsets: every [M, K]
+# operand and [M, N] output must stay below 2 GiB (the binding refuses larger ones).  Larger GEMMs run
+# as row chunks (GPT-2 124M at micro-batch >= ~342, XL's d_ff = 6400 past ~168K rows), each chunk a
+# whole number of sequences for epilogue 3.
+_OFFSET_LIMIT = 2**31
+
+
+def _gemm_rows(a, b, b_kn: bool, epilogue: int, bias=None, u=None, dbias=None, seq_len: int = 0):
+    """``hip_ops().gemm_fused`` over row chunks small enough for its 32-bit offsets."""
+    m, k = a.shape
+    n = b.shape[1] if b_kn else b.shape[0]
+    align = 256 * seq_len if epilogue == 3 else 256
+    rows = max(align, (_OFFSET_LIMIT - 1) // (2 * max(k, n)) // align * align)
+    extra = () if epilogue < 3 else (seq_len,)
+    if m <= rows:
+        return tuple(hip_ops().gemm_fused(a, b, b_kn, epilogue, bias, u, dbias, *extra))
+    parts = [
+        hip_ops().gemm_fused(a[r0 : r0 + rows], b, b_kn, epilogue, bias,
+                             None if u is None else u[r0 : r0 + rows], dbias, *extra)
+        for r0 in range(0, m, rows)
+    ]
+    out = torch.cat([p[0] for p in parts])
+    if parts[0][1] is None:
+        return out, None
+    return out, torch.cat([p[1] for p in parts])
 
 
 def linear_fwd(x, w, bias=None):
     """``x @ w^T + bias`` (nn.Linear forward, bf16 out).  GPU: the fused MFMA GEMM with the bias in
     its epilogue where the shape allows, else hipBLASLt."""
     if _on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x, x.shape[1], w.shape[0], w, bias, op="fwd"):
-        return hip_ops().gemm_fused(x, w, False, 0, bias)[0]
+        return _gemm_rows(x, w, False, 0, bias)[0]
     return torch.mm(x, w.t()) if bias is None else torch.addmm(bias, x, w.t())
 
 
@@ -235,7 +304,7 @@ def linear_fwd_gelu(x, w, bias=None):
     """``u = x @ w^T + bias`` and ``g = gelu(u)`` (exact erf GELU of the bf16 ``u``, which the
     backward reads): on GPU the GELU rides in the GEMM epilogue, no separate pass over ``u``."""
     if _on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x, x.shape[1], w.shape[0], w, bias, op="fwd_gelu"):
-        u, g = hip_ops().gemm_fused(x, w, False, 1, bias)
+        u, g = _gemm_rows(x, w, False, 1, bias)
         return u, g
     u = torch.mm(x, w.t()) if bias is None else torch.addmm(bias, x, w.t())
     return u, gelu_fwd(u)
@@ -244,7 +313,7 @@ def linear_fwd_gelu(x, w, bias=None):
 def linear_dx(dy, w):
     """``dy @ w`` (data gradient of nn.Linear with weight ``w [out, in]``)."""
     if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy, dy.shape[1], w.shape[1], w, op="dx"):
-        return hip_ops().gemm_fused(dy, w, True, 0)[0]
+        return _gemm_rows(dy, w, True, 0)[0]
     return torch.mm(dy, w)
 
 
@@ -283,7 +352,7 @@ def linear_dx_gelu_bwd(dy, w, u, dbias=None):
     projection fused with the GELU backward and the fc bias gradient (one GEMM epilogue on GPU
     instead of a GEMM plus a full read-modify pass over the [M, d_ff] activations)."""
     if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy, dy.shape[1], w.shape[1], w, u, op="dx_gelu"):
-        return hip_ops().gemm_fused(dy, w, True, 2, None, u, dbias)[0]
+        return _gemm_rows(dy, w, True, 2, None, u, dbias)[0]
     return gelu_bwd(torch.mm(dy, w), u, dbias)
 
 
@@ -303,7 +372,9 @@ def linear_dx_attn(dy, w, att, seqlen: int, v_bias_grad=None, head_dim: int = 64
         and w.shape[1] % 64 == 0
         and _fgemm_ok(dy, dy.shape[1], w.shape[1], w, att, op="dx_attn")
     ):
-        return tuple(hip_ops().gemm_fused(dy, w, True, 3, None, att, v_bias_grad, seqlen))
+        return _gemm_rows(dy, w, True, 3, None, att, v_bias_grad, seqlen)
+    if _on_gpu(dy) and head_dim != 64:
+        _det_fallback(f"attention out-projection dX at head_dim={head_dim}")
     return torch.mm(dy, w), None
 
 

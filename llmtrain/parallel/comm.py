@@ -38,8 +38,11 @@ __all__ = [
     "TransportSummary",
     "check_transport",
     "configure_rccl_env",
+    "current_transport",
     "last_probe",
     "probe_allreduce",
+    "rccl_report",
+    "relay_warnings",
     "summarize_transport",
 ]
 
@@ -52,7 +55,7 @@ WARN_BUSBW_GBPS = 40.0
 _TRANSPORT_RE = re.compile(r"via (P2P(?:/[\w.]+)?|SHM(?:/[\w.]+)*|NET/[\w.]+|COLLNET\S*)")
 _CHANNELS_RE = re.compile(r"(\d+) coll channels")
 
-_state: dict[str, Any] = {"probe": None, "debug_file": None}
+_state: dict[str, Any] = {"probe": None, "debug_file": None, "relayed": 0}
 
 
 @dataclass(frozen=True)
@@ -82,17 +85,27 @@ class TransportSummary:
         return any(self.counts.get(k, 0) for k in ("SHM", "NET"))
 
 
-def configure_rccl_env(extra: dict[str, Any], rank: int) -> str | None:
+def configure_rccl_env(extra: dict[str, Any], rank: int, default_dir: str | os.PathLike[str] | None = None) -> str | None:
     """Set RCCL environment knobs before the process group exists; returns the debug-file path
-    (None when the operator owns ``NCCL_DEBUG`` or ``ddp.extra.log_transport`` is false)."""
+    (None when the operator owns ``NCCL_DEBUG`` or ``ddp.extra.log_transport`` is false).
+
+    The file lives under ``ddp.extra.transport_log_dir``, else ``default_dir`` (the run's
+    ``output.root_dir``/``rccl``: on the runs PVC in Kubernetes, so it outlives the pod), else the
+    temp directory.  ``NCCL_DEBUG_FILE`` takes ALL of RCCL's output, warnings included, so
+    :func:`relay_warnings` copies its ``WARN`` lines to the log (stderr) at startup and teardown."""
     for key, env in (("max_channels", "NCCL_MAX_NCHANNELS"), ("min_channels", "NCCL_MIN_NCHANNELS")):
         if extra.get(key) is not None:
             os.environ[env] = str(int(extra[key]))
     _state["debug_file"] = None
     if not bool(extra.get("log_transport", True)) or "NCCL_DEBUG" in os.environ:
         return None
-    root = Path(extra.get("transport_log_dir") or tempfile.gettempdir())
+    root = Path(extra.get("transport_log_dir") or default_dir or tempfile.gettempdir())
+    try:
+        root.mkdir(parents=True, exist_ok=True)
+    except OSError:
+        root = Path(tempfile.gettempdir())
     path = root / f"llmtrain-rccl-rank{rank}-{os.getpid()}.log"
+    _state["relayed"] = 0
     os.environ["NCCL_DEBUG"] = "INFO"
     os.environ.setdefault("NCCL_DEBUG_SUBSYS", "INIT,GRAPH")
     os.environ["NCCL_DEBUG_FILE"] = str(path)
@@ -118,6 +131,21 @@ def summarize_transport(path: str | os.PathLike[str] | None, *, keep_lines: int 
             if len(summary.lines) < keep_lines:
                 summary.lines.append(line.strip())
     return summary
+
+
+def relay_warnings(path: str | os.PathLike[str] | None = None) -> list[str]:
+    """Log (WARNING, to stderr) every ``WARN`` line RCCL wrote to its debug file since the last
+    call — transport errors and watchdog timeouts would otherwise only be in that file."""
+    path = path or _state["debug_file"]
+    if path is None or not Path(path).exists():
+        return []
+    lines = Path(path).read_text(errors="replace").splitlines()
+    start = int(_state.get("relayed") or 0)
+    _state["relayed"] = len(lines)
+    warns = [ln.strip() for ln in lines[start:] if " WARN " in ln or "NCCL WARN" in ln]
+    for ln in warns:
+        logger.warning("rccl: %s", ln)
+    return warns
 
 
 def _sync(device: torch.device) -> None:
@@ -156,6 +184,22 @@ def probe_allreduce(
     return result
 
 
+def current_transport() -> TransportSummary:
+    """:func:`summarize_transport` of this process's RCCL debug file (empty without one)."""
+    return summarize_transport(_state["debug_file"])
+
+
+def rccl_report() -> dict[str, Any]:
+    """What a multi-GPU result needs to explain itself: the transports RCCL connected its channels
+    with, the channel count, whether any fell back to SHM / NET, and the channel / algorithm env
+    knobs in force (``ddp.extra.max_channels`` etc.)."""
+    t = current_transport()
+    env = {k: os.environ[k] for k in ("NCCL_MAX_NCHANNELS", "NCCL_MIN_NCHANNELS", "NCCL_ALGO", "NCCL_PROTO")
+           if k in os.environ}
+    return {"transport_counts": dict(t.counts), "channels": t.channels, "fallback": t.fallback, "env": env,
+            "debug_file": _state["debug_file"]}
+
+
 def last_probe() -> BusBandwidth | None:
     """The result of the most recent :func:`probe_allreduce` in this process (None before)."""
     return _state["probe"]
@@ -175,6 +219,7 @@ def check_transport(device: torch.device, extra: dict[str, Any], *, rank: int) -
                 probe.ms_per_iter, probe.backend,
             )
     summary = summarize_transport(_state["debug_file"])
+    relay_warnings()
     if rank == 0 and (summary.counts or summary.channels is not None):
         logger.info("rccl transport: %s channels=%s", summary.counts, summary.channels)
         for line in summary.lines:

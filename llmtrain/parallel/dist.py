@@ -13,6 +13,7 @@ import logging
 import os
 from dataclasses import dataclass
 from datetime import timedelta
+from pathlib import Path
 
 import torch
 import torch.distributed as dist
@@ -90,7 +91,7 @@ def setup_ddp(cfg: RunConfig) -> DDPState:
     backend = resolve_backend(cfg)
     kwargs = {}
     if backend == "nccl":
-        comm.configure_rccl_env(cfg.ddp.extra, rank)
+        comm.configure_rccl_env(cfg.ddp.extra, rank, default_dir=Path(cfg.output.root_dir) / "rccl")
     probe_device = torch.device("cpu")
     if _uses_gpu(cfg) and torch.cuda.is_available():
         # local_rank modulo the visible devices, as runtime/device.py picks the device: identity on a
@@ -122,6 +123,7 @@ def setup_ddp(cfg: RunConfig) -> DDPState:
 
 
 def teardown_ddp() -> None:
+    comm.relay_warnings()
     if dist.is_initialized():
         logger.info("Destroying DDP process group")
         dist.destroy_process_group()

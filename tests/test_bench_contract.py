@@ -79,6 +79,13 @@ def test_bench_gpus_2_spawns_two_ranks() -> None:
     assert len(res["per_rank_tokens_per_sec"]) == 2 and len(res["exposed_allreduce_ms"]) == 2
     assert res["config"]["global_batch"] == 2 * 2
     assert res["value"] > 0 and res["steps"] == 2 and res["warmup"] == 1
+    # a multi-rank line explains itself: RCCL transports / channels (empty on gloo) and the
+    # exposed tail bucket (the tied embedding) with its queue and collective times
+    assert set(res["rccl"]) >= {"transport_counts", "channels", "fallback", "env"}
+    if res.get("buckets_rank0"):
+        assert res["tail_bucket"]["bucket"] == res["buckets_rank0"][-1]["bucket"]
+        # (queue / collective times come from GPU events: on the CPU gloo path only the payload)
+        assert res["tail_bucket"]["payload_mib"] == res["buckets_rank0"][-1]["payload_mib"]
 
 
 def test_bench_rejects_world_size_mismatch() -> None:

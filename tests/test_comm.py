@@ -101,3 +101,26 @@ def test_configure_rccl_env_respects_operator(monkeypatch: pytest.MonkeyPatch, t
     assert os.environ["NCCL_DEBUG"] == "INFO" and os.environ["NCCL_MAX_NCHANNELS"] == "8"
     monkeypatch.setenv("NCCL_DEBUG", "WARN")  # the operator's setting wins
     assert comm.configure_rccl_env({}, rank=0) is None and os.environ["NCCL_DEBUG"] == "WARN"
+
+
+def test_rccl_debug_file_defaults_to_run_volume_and_relays_warnings(
+    monkeypatch: pytest.MonkeyPatch, tmp_path: Path
+) -> None:
+    """NCCL_DEBUG_FILE swallows RCCL's warnings too: the file defaults to the run root (the PVC in
+    Kubernetes, not the pod's /tmp) and its WARN lines are re-logged at startup / teardown."""
+    for key in ("NCCL_DEBUG", "NCCL_DEBUG_FILE", "NCCL_DEBUG_SUBSYS"):
+        monkeypatch.delenv(key, raising=False)
+    path = comm.configure_rccl_env({}, rank=1, default_dir=tmp_path / "rccl")
+    assert path is not None and Path(path).parent == tmp_path / "rccl"
+    Path(path).write_text(
+        "h:1:1 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[1] via P2P/IPC\n"
+        "h:1:1 [0] NCCL WARN Call to ibv_open_device failed\n"
+    )
+    logged: list[str] = []
+    monkeypatch.setattr(comm.logger, "warning", lambda fmt, *a: logged.append(fmt % a))
+    assert comm.relay_warnings() == ["h:1:1 [0] NCCL WARN Call to ibv_open_device failed"]
+    assert comm.relay_warnings() == []  # already relayed
+    with open(path, "a") as fh:
+        fh.write("h:1:1 [0] NCCL WARN watchdog timeout\n")
+    assert comm.relay_warnings() == ["h:1:1 [0] NCCL WARN watchdog timeout"]
+    assert sum("NCCL WARN" in line for line in logged) == 2

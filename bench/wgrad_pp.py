@@ -1,0 +1,110 @@
+"""Weight-gradient GEMM: ping-pong kernel (csrc/gemm_wgrad_pp.hip) vs the round-3 kernels.
+
+    python bench/wgrad_pp.py check            # numerics vs fp32 (every shape, bias, strided dy)
+    python bench/wgrad_pp.py time [--tokens M] [--model gpt2-124m|gpt2-xl|head]
+
+Each timing line: kernel, shape, ms (median of 20), TFLOP/s on the 2*M*N*K GEMM FLOPs.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from micro import timeit  # noqa: E402
+
+SHAPES = {
+    "gpt2-124m": {"qkv": (2304, 768), "out": (768, 768), "fc": (3072, 768), "proj": (768, 3072)},
+    "gpt2-xl": {"qkv": (4800, 1600), "out": (1600, 1600), "fc": (6400, 1600), "proj": (1600, 6400)},
+    "head": {"head": (50257, 768)},
+}
+
+
+def _ops():
+    from llmtrain.ops import _ext
+
+    _ext.require()
+    return torch.ops.llmtrain_hip
+
+
+def check() -> int:
+    ops = _ops()
+    torch.manual_seed(0)
+    bad = 0
+    cases = [(4096, n, k, name) for model in ("gpt2-124m", "gpt2-xl") for name, (n, k) in SHAPES[model].items()]
+    cases += [(1000, 2304, 768, "ragged M"), (3 * 32 + 5, 768, 768, "tiny M"), (2048, 50257, 768, "head")]
+    for M, N, K, name in cases:
+        for mode in (-1, 0, 2):
+            lda = 50304 if N == 50257 else N
+            base = torch.randn(M, lda, device="cuda", dtype=torch.bfloat16)
+            dy = base[:, :N]
+            x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+            c0 = torch.randn(N, K, device="cuda")
+            b0 = torch.randn(N, device="cuda")
+            c, b = c0.clone(), b0.clone()
+            ops.wgrad_gemm_pp(dy, x, c, b, 0, mode)
+            ref = c0 + dy.float().t() @ x.float()
+            rb = b0 + dy.float().sum(0)
+            err = ((c - ref).abs().max() / ref.abs().max()).item()
+            berr = ((b - rb).abs().max() / rb.abs().max()).item()
+            ok = err < 2e-5 and berr < 2e-5
+            bad += not ok
+            print(json.dumps({"case": name, "M": M, "N": N, "K": K, "mode": mode, "rel_err": err, "bias_rel_err": berr,
+                              "ok": ok}), flush=True)
+    # run-to-run bitwise (slab mode)
+    dy = torch.randn(8192, 2304, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(8192, 768, device="cuda", dtype=torch.bfloat16)
+    outs = []
+    for _ in range(3):
+        c = torch.zeros(2304, 768, device="cuda")
+        ops.wgrad_gemm_pp(dy, x, c, None, 0, 0)
+        outs.append(c)
+    same = all(torch.equal(outs[0], o) for o in outs[1:])
+    bad += not same
+    print(json.dumps({"case": "slab mode bitwise repeat", "ok": same}), flush=True)
+    return 1 if bad else 0
+
+
+def time_shapes(model: str, M: int) -> None:
+    ops = _ops()
+    for name, (N, K) in SHAPES[model].items():
+        lda = 50304 if N == 50257 else N
+        dy = torch.randn(M, lda, device="cuda", dtype=torch.bfloat16)[:, :N]
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        acc = torch.zeros(N, K, device="cuda")
+        bias = torch.zeros(N, device="cuda")
+        flops = 2.0 * M * N * K
+        variants = {
+            "r3_tile256": lambda: ops.wgrad_gemm(dy, x, acc, 0, 256, 0),
+            "r3_pipe": lambda: ops.wgrad_gemm(dy, x, acc, 0, 256, 4),
+            "pp_auto": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, -1),
+            "pp_slab": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, 0),
+            "pp_atomic": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, 2),
+            "pp_slab_bias": lambda: ops.wgrad_gemm_pp(dy, x, acc, bias, 0, 0),
+        }
+        for label, fn in variants.items():
+            ms = timeit(fn)
+            print(json.dumps({"model": model, "M": M, "gemm": name, "variant": label, "ms": round(ms, 4),
+                              "TFLOPs": round(flops / ms / 1e9, 1)}), flush=True)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", choices=["check", "time"])
+    ap.add_argument("--tokens", type=int, default=131072)
+    ap.add_argument("--model", default="gpt2-124m", choices=sorted(SHAPES))
+    args = ap.parse_args()
+    if args.what == "check":
+        return check()
+    time_shapes(args.model, args.tokens)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <vector>
 
 #include "kernels.h"
 
@@ -110,10 +111,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> add_layernorm_fwd(const Tensor& x, co
   return {xs, y, mean, rstd};
 }
 
-std::tuple<Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor& xs, const Tensor& mean, const Tensor& rstd,
-                                         const Tensor& w, const c10::optional<Tensor>& dresid, Tensor dw, Tensor db,
-                                         const c10::optional<Tensor>& dy_scale, bool want_lowp,
-                                         const c10::optional<Tensor>& dproj, double dropout_p, int64_t dropout_seed) {
+std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_impl(const Tensor& dy, const Tensor& xs, const Tensor& mean,
+                                                      const Tensor& rstd, const Tensor& w,
+                                                      const c10::optional<Tensor>& dresid, Tensor dw, Tensor db,
+                                                      const c10::optional<Tensor>& dy_scale, bool want_lowp,
+                                                      const c10::optional<Tensor>& dproj, double dropout_p,
+                                                      int64_t dropout_seed, bool defer_params) {
   check_gpu(dy, "dy");
   check_gpu(xs, "xs");
   check_dtype(xs, at::kFloat, "xs");
@@ -165,12 +168,62 @@ std::tuple<Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor& xs, con
   a.M = (int)M;
   a.d = (int)d;
   a.dropout = make_dropout(dropout_p, dropout_seed);
+  a.defer_params = defer_params;
+  TORCH_CHECK(!(defer_params && a.dproj != nullptr), "layernorm_bwd: deferred reduce takes no dproj_bias");
+  Tensor parts = at::empty({0}, xs.options());
   if (M > 0) {
     Tensor ws = workspace(xs, llmt::layernorm_bwd_ws_floats(a));
     a.ws = ws.data_ptr<float>();
     check_hip(llmt::launch_layernorm_bwd(a, cur_stream()), "layernorm_bwd");
+    // [2 (dw, db), grid, d] partial rows at the front of the workspace
+    if (defer_params) parts = ws.narrow(0, 0, 2L * llmt::layernorm_bwd_grid(a) * d).view({2, -1, d});
   }
-  return {dx, dx_lp};
+  return {dx, dx_lp, parts};
+}
+
+std::tuple<Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor& xs, const Tensor& mean, const Tensor& rstd,
+                                         const Tensor& w, const c10::optional<Tensor>& dresid, Tensor dw, Tensor db,
+                                         const c10::optional<Tensor>& dy_scale, bool want_lowp,
+                                         const c10::optional<Tensor>& dproj, double dropout_p, int64_t dropout_seed) {
+  auto r = layernorm_bwd_impl(dy, xs, mean, rstd, w, dresid, dw, db, dy_scale, want_lowp, dproj, dropout_p,
+                              dropout_seed, false);
+  return {std::get<0>(r), std::get<1>(r)};
+}
+
+// LayerNorm backward that leaves its dgamma / dbeta partial rows to a later batched reduce
+// (ln_param_reduce): returns (dx, dx_lowp, parts [2, grid, d])
+std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_deferred(const Tensor& dy, const Tensor& xs, const Tensor& mean,
+                                                          const Tensor& rstd, const Tensor& w,
+                                                          const c10::optional<Tensor>& dresid, Tensor dw, Tensor db,
+                                                          const c10::optional<Tensor>& dy_scale, bool want_lowp,
+                                                          double dropout_p, int64_t dropout_seed) {
+  return layernorm_bwd_impl(dy, xs, mean, rstd, w, dresid, dw, db, dy_scale, want_lowp, c10::nullopt, dropout_p,
+                            dropout_seed, true);
+}
+
+// dst[j] += sum over rows of parts[j // 2][j % 2] for every deferred LayerNorm: ONE launch for up to
+// two LayerNorms of equal (grid, d) (a block's ln_2 and ln_1), fixed order as in layernorm_bwd
+void ln_param_reduce(const std::vector<Tensor>& parts, std::vector<Tensor> dst) {
+  TORCH_CHECK(!parts.empty() && parts.size() <= 2 && dst.size() == 2 * parts.size(),
+              "ln_param_reduce: 1-2 parts tensors and 2 destinations each");
+  const int64_t grid = parts[0].size(1), d = parts[0].size(2);
+  const float* p[4];
+  float* o[4];
+  for (size_t i = 0; i < parts.size(); ++i) {
+    TORCH_CHECK(parts[i].dim() == 3 && parts[i].size(0) == 2 && parts[i].size(1) == grid && parts[i].size(2) == d,
+                "ln_param_reduce: parts must be [2, grid, d] of one shape");
+    for (int j = 0; j < 2; ++j) {
+      Tensor& t = dst[2 * i + j];
+      check_dtype(t, at::kFloat, "ln_param_reduce dst");
+      TORCH_CHECK(t.numel() == d && t.is_contiguous(), "ln_param_reduce: dst must be [d]");
+      p[2 * i + j] = parts[i].data_ptr<float>() + (long)j * grid * d;
+      o[2 * i + j] = t.data_ptr<float>();
+    }
+  }
+  const int njobs = (int)(2 * parts.size());
+  Tensor scratch = workspace(parts[0], (long)njobs * llmt::colsum_scratch_floats((int)grid, d));
+  check_hip(llmt::launch_colsum_reduce_multi(p, o, njobs, (int)grid, d, scratch.data_ptr<float>(), cur_stream()),
+            "ln_param_reduce");
 }
 
 // ---- cross-entropy ---------------------------------------------------------------------------
@@ -447,6 +500,36 @@ void wgrad_gemm(const Tensor& dy, const Tensor& x, Tensor c, int64_t split, int6
             "wgrad_gemm");
 }
 
+// dst[N, K] (fp32) += dy[M, N]^T x[M, K], and bias[N] += colsum(dy) when given (ping-pong kernel)
+void wgrad_gemm_pp(const Tensor& dy, const Tensor& x, Tensor c, const c10::optional<Tensor>& bias, int64_t split,
+                   int64_t mode) {
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && c.is_cuda(), "wgrad_gemm_pp: GPU tensors required");
+  check_dtype(dy, at::kBFloat16, "dy");
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(c, at::kFloat, "c");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && c.dim() == 2, "wgrad_gemm_pp: 2D operands");
+  TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1 && c.stride(1) == 1, "wgrad_gemm_pp: unit inner stride");
+  const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
+  TORCH_CHECK(x.size(0) == M && c.size(0) == N && c.size(1) == K, "wgrad_gemm_pp: shape mismatch");
+  TORCH_CHECK((uintptr_t)dy.data_ptr() % 16 == 0 && (uintptr_t)x.data_ptr() % 16 == 0,
+              "wgrad_gemm_pp: operands must be 16-byte aligned");
+  float* bptr = nullptr;
+  if (bias.has_value()) {
+    check_gpu(*bias, "bias");
+    check_dtype(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == N, "wgrad_gemm_pp: bias must have N elements");
+    bptr = bias->data_ptr<float>();
+  }
+  at::hip::HIPGuardMasqueradingAsCUDA guard(c.device());
+  const long wsf = llmt::wgrad_pp_ws_floats((int)dy.stride(0), (int)x.stride(0), (int)M, (int)N, (int)K, (int)split,
+                                            (int)mode, bptr != nullptr);
+  Tensor ws = workspace(c, wsf);
+  check_hip(llmt::launch_wgrad_pp(dy.data_ptr(), (int)dy.stride(0), x.data_ptr(), (int)x.stride(0),
+                                  c.data_ptr<float>(), (int)c.stride(0), (int)M, (int)N, (int)K, (int)split, (int)mode,
+                                  wsf > 0 ? ws.data_ptr<float>() : nullptr, bptr, cur_stream()),
+            "wgrad_gemm_pp");
+}
+
 // ---- fused forward / dX GEMM ------------------------------------------------------------------
 // out = epi(a @ op(b)): b is [N, K] (weight, forward) or, with b_kn, [K, N] (weight in dX = dy @ W).
 // epilogue 0 -> (out, None); 1 -> (u, gelu(u)); 2 -> (du = acc * gelu'(u), None) with dbias += colsum.
@@ -607,6 +690,10 @@ TORCH_LIBRARY(llmtrain_hip, m) {
   m.def("layernorm_bwd(Tensor dy, Tensor xs, Tensor mean, Tensor rstd, Tensor weight, Tensor? dresid,"
         " Tensor(a!) dweight, Tensor(b!) dbias, Tensor? dy_scale, bool want_lowp, Tensor(c!)? dproj_bias,"
         " float dropout_p=0., int dropout_seed=0) -> (Tensor, Tensor)");
+  m.def("layernorm_bwd_deferred(Tensor dy, Tensor xs, Tensor mean, Tensor rstd, Tensor weight, Tensor? dresid,"
+        " Tensor(a!) dweight, Tensor(b!) dbias, Tensor? dy_scale, bool want_lowp, float dropout_p=0.,"
+        " int dropout_seed=0) -> (Tensor, Tensor, Tensor)");
+  m.def("ln_param_reduce(Tensor[] parts, Tensor(a!)[] dst) -> ()");
   m.def("cross_entropy_fwd_bwd(Tensor(a!) logits, Tensor labels, int vocab, Tensor row_weight) -> Tensor");
   m.def("gelu_fwd(Tensor u) -> Tensor");
   m.def("scale(Tensor x, Tensor s) -> Tensor");
@@ -624,6 +711,7 @@ TORCH_LIBRARY(llmtrain_hip, m) {
   m.def("get_deterministic() -> bool", &get_deterministic);
   m.def("set_dropout_seed_offset(Tensor? word) -> ()", &set_dropout_seed_offset);
   m.def("wgrad_gemm(Tensor dy, Tensor x, Tensor(a!) c, int split=0, int tile=0, int pipe=-1) -> ()");
+  m.def("wgrad_gemm_pp(Tensor dy, Tensor x, Tensor(a!) c, Tensor(b!)? bias=None, int split=0, int mode=-1) -> ()");
   m.def("gemm_fused(Tensor a, Tensor b, bool b_kn, int epilogue, Tensor? bias=None, Tensor? u=None,"
         " Tensor(a!)? dbias=None, int seq_len=0) -> (Tensor, Tensor?)");
   m.def("sumsq(Tensor x) -> Tensor");
@@ -637,6 +725,8 @@ TORCH_LIBRARY(llmtrain_hip, m) {
 TORCH_LIBRARY_IMPL(llmtrain_hip, CUDA, m) {
   m.impl("add_layernorm_fwd", &add_layernorm_fwd);
   m.impl("layernorm_bwd", &layernorm_bwd);
+  m.impl("layernorm_bwd_deferred", &layernorm_bwd_deferred);
+  m.impl("ln_param_reduce", &ln_param_reduce);
   m.impl("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd);
   m.impl("gelu_fwd", &gelu_fwd);
   m.impl("scale", &scale);
@@ -648,6 +738,7 @@ TORCH_LIBRARY_IMPL(llmtrain_hip, CUDA, m) {
   m.impl("attn_bwd", &attn_bwd);
   m.impl("dropout_mask", &dropout_mask);
   m.impl("wgrad_gemm", &wgrad_gemm);
+  m.impl("wgrad_gemm_pp", &wgrad_gemm_pp);
   m.impl("gemm_fused", &gemm_fused);
   m.impl("sumsq", &sumsq);
   m.impl("adamw_flat", &adamw_flat);

@@ -57,7 +57,11 @@ struct LnBwdArgs {
   int M, d;
   DropoutArgs dropout;   // mask of the branch that fed this stream: applied to dx_lp and dproj
   float* ws;             // layernorm_bwd_ws_floats(*this) floats: partial rows of dw / db / dproj
+  bool defer_params;     // leave the dw / db partial rows in ws (layernorm_bwd_grid rows each) for a
+                         // later batched reduce (launch_colsum_reduce_multi) instead of reducing now
 };
+// partial rows per accumulated parameter vector (the backward's grid)
+int layernorm_bwd_grid(const LnBwdArgs& a);
 // dw, db, dproj are reduced over rows through per-workgroup partial rows in `ws` and a fixed-order
 // reduce (no atomics); the workspace size depends on M, d, the dtypes and whether dproj is set
 long layernorm_bwd_ws_floats(const LnBwdArgs& a);
@@ -143,6 +147,13 @@ hipError_t launch_sumsq(const float* x, long long n, float* partials, float* out
 // Deterministic mode: `det_ws` (wgrad_gemm_det_ws_floats(...) floats) receives per-chunk partial
 // slabs that are reduced into C in a fixed order instead of the split-K atomics.
 long wgrad_gemm_det_ws_floats(int lda, int ldb, int M, int N, int K, int split, int tile);
+
+// Ping-pong weight-gradient GEMM (gemm_wgrad_pp.hip): C[N,K] += dy^T x and, with `bias`,
+// bias[N] += colsum(dy).  `ws` holds wgrad_pp_ws_floats(...) floats (split slabs + bias parts).
+// mode: -1 auto, 0 slabs + fixed-order reduce, 2 fp32 atomics (ignored in deterministic mode).
+long wgrad_pp_ws_floats(int lda, int ldb, int M, int N, int K, int split, int mode, bool bias);
+hipError_t launch_wgrad_pp(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N, int K,
+                           int split, int mode, float* ws, float* bias, hipStream_t stream);
 // `pipe`: 0 = the plain 256-tile kernel (332 registers per lane: other kernels' waves can share
 // its SIMDs — the side-stream default), 4 / 5 = the software-pipelined one with that many ring
 // slots (all 512 registers: nothing else runs beside it — for GEMMs that own the chip), -1 = the

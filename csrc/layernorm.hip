@@ -443,6 +443,7 @@ void launch_bwd_c(const LnBwdArgs& a, hipStream_t st) {
   void* args[] = {&dy, &xs, &mean, &rstd, &w, &dresid, &dy_scale, &dx, &dx_lp, &pw, &pb, &pp, &M, &d, &dr};
   (void)hipLaunchKernel(fn, dim3(grid), dim3(256), args, shm, st);
 
+  if (a.defer_params) return;  // the caller reduces dw / db later, batched with other LayerNorms
   const int nacc = a.dproj != nullptr ? 3 : 2;
   float* scratch = a.ws + (long)nacc * grid * a.d;
   const float* parts[3] = {pw, pb, pp};
@@ -481,6 +482,23 @@ namespace {
 template <int MAXC>
 void grid_c(const LnBwdArgs& a, int& out) { out = bwd_grid_c<MAXC>(a); }
 }  // namespace
+
+int layernorm_bwd_grid(const LnBwdArgs& a) {
+  if (a.d % 4 != 0 || a.M <= 0) return 0;
+  int grid = 0;
+  switch ((a.d / 4 + 63) / 64) {
+    case 1: grid_c<1>(a, grid); break;
+    case 2: grid_c<2>(a, grid); break;
+    case 3: grid_c<3>(a, grid); break;
+    case 4: grid_c<4>(a, grid); break;
+    case 5: grid_c<5>(a, grid); break;
+    case 6: grid_c<6>(a, grid); break;
+    case 7: grid_c<7>(a, grid); break;
+    case 8: grid_c<8>(a, grid); break;
+    default: return 0;
+  }
+  return grid;
+}
 
 long layernorm_bwd_ws_floats(const LnBwdArgs& a) {
   if (a.d % 4 != 0 || a.M <= 0) return 0;

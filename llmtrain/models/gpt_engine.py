@@ -213,23 +213,26 @@ class FusedGPTEngine:
     def _g(self, p: torch.Tensor) -> torch.Tensor:
         return self.store.grad_of(p)
 
-    def _wgrad(self, dst: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
-        """Block weight gradients: the split-K MFMA kernel (``ops.wgrad_accum``) on GPU — it fills
-        the chip on these M-deep reductions where hipBLASLt picks too few tiles.  On GPU it runs
-        on the side stream after an event on the main stream (``dy``/``x`` are ready); the engine
-        holds ``dy``/``x`` until the main stream has fenced the GEMM (:meth:`_retire_block`), so
-        their memory is not reused before the side stream is done with it."""
+    def _wgrad(self, dst: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, bias: torch.Tensor | None = None) -> None:
+        """Block weight (and bias: ``bias += colsum(dy)``) gradients: the split-K MFMA kernel
+        (``ops.wgrad_accum``) on GPU — it fills the chip on these M-deep reductions where hipBLASLt
+        picks too few tiles, and sums the bias columns from the ``dy`` tiles it streams anyway.  On
+        GPU it runs on the side stream after an event on the main stream (``dy``/``x`` are ready);
+        the engine holds ``dy``/``x`` until the main stream has fenced the GEMM
+        (:meth:`_retire_block`), so their memory is not reused before the side stream is done."""
         if not (dst.is_cuda and dy.dtype == torch.bfloat16):
             accumulate_wgrad(dst, dy, x)
+            if bias is not None:
+                ops.colsum_accum(dy, bias)
             return
         side = self._side_stream()
         if side is not None:
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
-                ops.wgrad_accum(dst, dy, x)
+                ops.wgrad_accum(dst, dy, x, bias=bias)
             self._pending.extend((dy, x))
-        else:  # one stream: nothing runs beside it, so the 512-register pipelined kernel
-            ops.wgrad_accum(dst, dy, x, exclusive=True)
+        else:  # one stream: nothing runs beside it
+            ops.wgrad_accum(dst, dy, x, bias=bias, exclusive=True)
 
     def _retire_block(self) -> None:
         """End of one block's backward: fence its side-stream GEMMs with an event and release the
@@ -411,7 +414,7 @@ class FusedGPTEngine:
         n_layers = len(self.blocks)
         dx, dx_lp = ops.layernorm_bwd(
             dhf, st.xf, st.muf, st.rsf, m.ln_f.weight, None, self._g(m.ln_f.weight), self._g(m.ln_f.bias),
-            go, want_lowp=True, dproj_bias=self._g(last.mlp_proj.bias), dropout=st.site(3 * n_layers),
+            go, want_lowp=True, dropout=st.site(3 * n_layers),
         )
         del dhf
         self._notify("ln_f")
@@ -420,62 +423,57 @@ class FusedGPTEngine:
         for i in reversed(range(len(self.blocks))):
             self._push(f"bwd.block{i}")
             blk, a = self.blocks[i], st.blocks[i]
-            # MLP: delta = g Wp^T + bp ; dx is d(delta) (bias grad already summed by the LN bwd)
-            self._wgrad(self._g(blk.mlp_proj.weight), dx_lp, a.g)
-            if self.fused_gemm:  # GELU backward + fc bias grad in the dX GEMM's epilogue
-                du = ops.linear_dx_gelu_bwd(dx_lp, self._w(blk.mlp_proj.weight), a.u, self._g(blk.mlp_fc.bias))
+            # MLP: delta = g Wp^T + bp ; dx is d(delta).  Every bias gradient of the block is the
+            # column sum of the output gradient its weight-gradient GEMM streams: summed there
+            self._wgrad(self._g(blk.mlp_proj.weight), dx_lp, a.g, self._g(blk.mlp_proj.bias))
+            if self.fused_gemm:  # GELU backward in the dX GEMM's epilogue
+                du = ops.linear_dx_gelu_bwd(dx_lp, self._w(blk.mlp_proj.weight), a.u)
             else:
                 dg = torch.mm(dx_lp, self._w(blk.mlp_proj.weight))
-                du = ops.gelu_bwd(dg, a.u, self._g(blk.mlp_fc.bias))
+                du = ops.gelu_bwd(dg, a.u, None)
                 del dg
-            self._wgrad(self._g(blk.mlp_fc.weight), du, a.h2)
+            self._wgrad(self._g(blk.mlp_fc.weight), du, a.h2, self._g(blk.mlp_fc.bias))
             wf = self._w(blk.mlp_fc.weight)
             dh2 = ops.linear_dx(du, wf) if self.fused_gemm else torch.mm(du, wf)
             del du
-            masked = st.keep_col is not None
-            dxm, dy_lp = ops.layernorm_bwd(
+            # ln_2's dgamma / dbeta partial rows wait for ln_1's: one reduce launch per block
+            dxm, dy_lp, ln2_parts = ops.layernorm_bwd(
                 dh2, a.xm, a.mu2, a.rs2, blk.ln_2.weight, dx, self._g(blk.ln_2.weight), self._g(blk.ln_2.bias),
-                None, want_lowp=True, dproj_bias=None if masked else self._g(blk.attn.out_proj.bias),
-                dropout=st.site(1 + 3 * i),
+                None, want_lowp=True, dropout=st.site(1 + 3 * i), defer_params=True,
             )
             del dh2, dx, dx_lp
-            if masked:  # gradient of y * keep: padded rows feed nothing back into the attention
+            if st.keep_col is not None:  # gradient of y * keep: padded rows feed nothing back
                 dy_lp = dy_lp * st.keep_col
-                ops.colsum_accum(dy_lp, self._g(blk.attn.out_proj.bias))
             # attention output projection
-            self._wgrad(self._g(blk.attn.out_proj.weight), dy_lp, a.att)
+            self._wgrad(self._g(blk.attn.out_proj.weight), dy_lp, a.att, self._g(blk.attn.out_proj.bias))
             wo = self._w(blk.attn.out_proj.weight)
             attn_drop = st.site(2 + 3 * i)
-            qkv_bg = self._g(blk.attn.qkv_proj.bias)
             delta = None
             if self.fused_gemm:
-                # dO plus the attention backward's row constants (and, without attention dropout,
-                # the V part of the qkv-bias gradient) from one GEMM epilogue
-                # (not taken -> delta None: attn_bwd computes it and the V-bias part itself)
-                d = qkv_bg.numel() // 3
-                datt, delta = ops.linear_dx_attn(
-                    dy_lp, wo, a.att, seqlen, v_bias_grad=qkv_bg[2 * d :] if attn_drop[0] == 0 else None,
-                    head_dim=self.head_dim,
-                )
+                # dO plus the attention backward's row constants from one GEMM epilogue
+                # (not taken -> delta None: attn_bwd computes them itself)
+                datt, delta = ops.linear_dx_attn(dy_lp, wo, a.att, seqlen, head_dim=self.head_dim)
             else:
                 datt = torch.mm(dy_lp, wo)
             del dy_lp
-            # the qkv-bias gradient (column sums of dqkv) is fused into the attention backward
             dqkv = ops.attn_bwd(
-                datt, a.qkv, a.att, a.lse, bsz, seqlen, self.n_heads, dropout=attn_drop,
-                qkv_bias_grad=qkv_bg, delta=delta, key_masks=st.key_masks,
+                datt, a.qkv, a.att, a.lse, bsz, seqlen, self.n_heads, dropout=attn_drop, delta=delta,
+                key_masks=st.key_masks,
             )
             del datt
-            self._wgrad(self._g(blk.attn.qkv_proj.weight), dqkv, a.h1)
+            self._wgrad(self._g(blk.attn.qkv_proj.weight), dqkv, a.h1, self._g(blk.attn.qkv_proj.bias))
             wq = self._w(blk.attn.qkv_proj.weight)
             dh1 = ops.linear_dx(dqkv, wq) if self.fused_gemm else torch.mm(dqkv, wq)
             del dqkv
-            prev_bias = self._g(self.blocks[i - 1].mlp_proj.bias) if i > 0 else None
-            dx, dx_lp = ops.layernorm_bwd(
+            dx, dx_lp, ln1_parts = ops.layernorm_bwd(
                 dh1, a.xs, a.mu1, a.rs1, blk.ln_1.weight, dxm, self._g(blk.ln_1.weight), self._g(blk.ln_1.bias),
-                None, want_lowp=i > 0, dproj_bias=prev_bias, dropout=st.site(3 * i) if i > 0 else (0.0, 0),
+                None, want_lowp=i > 0, dropout=st.site(3 * i) if i > 0 else (0.0, 0), defer_params=True,
             )
-            del dh1, dxm
+            ops.ln_param_reduce(
+                [ln2_parts, ln1_parts],
+                [self._g(blk.ln_2.weight), self._g(blk.ln_2.bias), self._g(blk.ln_1.weight), self._g(blk.ln_1.bias)],
+            )
+            del dh1, dxm, ln2_parts, ln1_parts
             st.blocks[i] = None  # type: ignore[call-overload]  # free activations early
             self._notify(f"block{i}")
             self._retire_block()

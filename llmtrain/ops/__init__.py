@@ -8,6 +8,8 @@ op and no silent fallback: a GPU tensor with the extension missing raises (``_ex
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from llmtrain.ops import _ext
@@ -33,10 +35,13 @@ __all__ = [
     "linear_dx_gelu_bwd",
     "linear_fwd",
     "linear_fwd_gelu",
+    "ln_param_reduce",
     "scale",
     "set_deterministic",
     "single_stream",
     "sumsq",
+    "wgrad_accum",
+    "wgrad_fuses_bias",
 ]
 
 
@@ -69,8 +74,6 @@ def set_deterministic(on: bool, schedule: str | None = None) -> bool:
     an order that depends on which workgroups finish first, which the weight-gradient side stream
     perturbs (bench/determinism_probe.py --runs, docs/round3.md).  Returns the previous setting.
     The CPU reference ops are deterministic anyway."""
-    import os
-
     schedule = schedule or os.environ.get("LLMTRAIN_DET_SCHEDULE", "serial")
     if schedule not in DET_SCHEDULES:
         raise ValueError(f"deterministic schedule must be one of {DET_SCHEDULES}, not {schedule!r}")
@@ -99,7 +102,7 @@ def add_layernorm_fwd(x, delta, weight, bias, eps: float, out_dtype: torch.dtype
 
 def layernorm_bwd(
     dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale=None, *, want_lowp=False, dproj_bias=None,
-    dropout=(0.0, 0),
+    dropout=(0.0, 0), defer_params=False,
 ):
     """LayerNorm backward with two optional fusions for the producer of the normalised input:
 
@@ -109,8 +112,23 @@ def layernorm_bwd(
 
     both see the branch's dropout mask ``dropout = (p, site_seed)`` (the fp32 ``dx`` of the
     residual stream itself does not).  Returns ``(dx_fp32, dx_lowp | None)``.
+
+    ``defer_params``: dgamma / dbeta are NOT accumulated yet; a third value ``parts`` (partial rows,
+    ``[2, rows, d]``) goes to :func:`ln_param_reduce`, which reduces two LayerNorms in one launch.
     """
     p, seed = dropout
+    if defer_params:
+        if dproj_bias is not None:
+            raise ValueError("layernorm_bwd: defer_params takes no dproj_bias")
+        if _on_gpu(dy):
+            dx, dx_lp, parts = hip_ops().layernorm_bwd_deferred(
+                dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale, want_lowp, p, seed
+            )
+            return dx, (dx_lp if want_lowp else None), parts
+        pw, pb = torch.zeros_like(dweight), torch.zeros_like(dbias)
+        dx = ref.layernorm_bwd(dy, xs, mean, rstd, weight, dresid, pw, pb, dy_scale)
+        branch = ref._apply_dropout(dx, p, seed)
+        return dx, (branch.to(dy.dtype) if want_lowp else None), torch.stack([pw, pb])[:, None, :]
     if _on_gpu(dy):
         dx, dx_lp = hip_ops().layernorm_bwd(
             dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale, want_lowp, dproj_bias, p, seed
@@ -121,6 +139,24 @@ def layernorm_bwd(
     if dproj_bias is not None:
         ref.colsum_accum(branch, dproj_bias)
     return dx, (branch.to(dy.dtype) if want_lowp else None)
+
+
+def ln_param_reduce(parts: list, dst: list) -> None:
+    """``dst[2i] += rows of parts[i][0]``, ``dst[2i + 1] += rows of parts[i][1]`` for the deferred
+    LayerNorm backwards of :func:`layernorm_bwd` — one fixed-order launch on GPU for LayerNorms with
+    equal partial-row counts (a block's ln_2 and ln_1), separate launches otherwise."""
+    if not parts:
+        return
+    if parts[0].device.type != "cuda":
+        for i, pr in enumerate(parts):
+            dst[2 * i] += pr[0].sum(0)
+            dst[2 * i + 1] += pr[1].sum(0)
+        return
+    if len({tuple(pr.shape) for pr in parts}) == 1:
+        hip_ops().ln_param_reduce(list(parts), list(dst))
+        return
+    for i, pr in enumerate(parts):
+        hip_ops().ln_param_reduce([pr], [dst[2 * i], dst[2 * i + 1]])
 
 
 def cross_entropy_fwd_bwd(logits, labels, vocab: int, row_weight):
@@ -378,17 +414,34 @@ def linear_dx_attn(dy, w, att, seqlen: int, v_bias_grad=None, head_dim: int = 64
     return torch.mm(dy, w), None
 
 
-def wgrad_accum(dst, dy, x, *, exclusive: bool = False) -> None:
-    """``dst (fp32 [N, K]) += dy[M, N]^T @ x[M, K]`` — split-K MFMA GEMM with atomic fp32
-    accumulation on GPU (``dy`` may be a column slice with a larger row stride).  ``exclusive``:
-    nothing runs beside this GEMM (the LM head's, on the main stream), so the software-pipelined
-    kernel that takes all 512 registers of every SIMD it lands on is used; side-stream weight
-    gradients keep the 332-register kernel so main-stream waves can share its CUs (with the
-    pipelined one the fc-bias column sum behind them waited ~490 us per layer)."""
+# Weight-gradient kernel: "pp" = the ping-pong kernel (csrc/gemm_wgrad_pp.hip: 8 waves, 2 per
+# SIMD, slab epilogue, bias column sums fused), "r3" = the round-3 kernels (csrc/gemm_wgrad.hip).
+WGRAD_KERNEL = os.environ.get("LLMTRAIN_WGRAD_KERNEL", "r3")
+
+
+def wgrad_fuses_bias() -> bool:
+    """True when :func:`wgrad_accum` computes ``bias += colsum(dy)`` inside the GEMM kernel (the
+    engine then drops the separate bias column sums of the producing kernels)."""
+    return WGRAD_KERNEL == "pp"
+
+
+def wgrad_accum(dst, dy, x, *, bias=None, exclusive: bool = False) -> None:
+    """``dst (fp32 [N, K]) += dy[M, N]^T @ x[M, K]`` and, with ``bias`` (fp32 ``[N]``),
+    ``bias += colsum(dy)`` — the weight and bias gradients of an nn.Linear whose output gradient
+    is ``dy`` (``dy`` may be a column slice with a larger row stride).
+
+    GPU: the split-K MFMA GEMM (:data:`WGRAD_KERNEL`).  With the round-3 kernels ``exclusive``
+    (nothing runs beside this GEMM: the LM head's, on the main stream) selects the 512-register
+    software-pipelined variant, and the bias is a separate column-sum pass."""
     if _on_gpu(dst):
+        if WGRAD_KERNEL == "pp":
+            hip_ops().wgrad_gemm_pp(dy, x, dst, bias, 0, -1)
+            return
         hip_ops().wgrad_gemm(dy, x, dst, 0, 0, 4 if exclusive else 0)
     else:
         dst.addmm_(dy.t().float(), x.float())
+    if bias is not None:
+        colsum_accum(dy, bias)
 
 
 def sumsq(x):

@@ -169,3 +169,51 @@ def test_fused_engine_mid_run_resume(gpu_device, tmp_path, dropout):
     assert resumed.resumed_from_step == 6 and resumed.final_step == 8
     print(f"resume: full {full.final_loss!r} resumed {resumed.final_loss!r}")
     assert abs(resumed.final_loss - full.final_loss) <= 1e-5 * abs(full.final_loss)
+
+
+def test_fused_step_at_benchmark_shape(gpu_device):
+    """One fused step with the benchmark's exact routing — micro-batch 128 x 1024 tokens, d 768,
+    12 heads, V 50257, so every GEMM takes its M = 131072 path (hipBLASLt above the fused-GEMM size
+    cap, the GELU / attention dX epilogues at any size, the per-(b, h) fp32-dQ attention backward at
+    B*H = 1536, the LM head's 50304-wide logits) — against fp32 autograd of the module path, with 2
+    layers instead of 12.  Bound: per-parameter relative gradient error (bf16 compute)."""
+    torch.manual_seed(0)
+    V, T, B = 50257, 1024, 128
+    ref_model = GPT(vocab_size=V, block_size=T, d_model=768, n_layers=2, n_heads=12, d_ff=3072, dropout=0.0)
+    ref_model = ref_model.to(gpu_device)
+    fused = copy.deepcopy(ref_model)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    ids = torch.randint(0, V, (B, T), generator=g).to(gpu_device)
+    labels = torch.randint(0, V, (B, T), generator=g).to(gpu_device)
+
+    ref_grads = {}
+    for i in range(0, B, 16):  # fp32 reference in slices of 16 sequences (the T x T scores are fp32)
+        logits = ref_model(ids[i : i + 16])
+        loss = F.cross_entropy(logits.reshape(-1, V), labels[i : i + 16].reshape(-1), reduction="sum") / (B * T)
+        loss.backward()
+        del logits, loss
+    loss_ref = 0.0
+    with torch.no_grad():
+        for i in range(0, B, 16):
+            loss_ref += F.cross_entropy(ref_model(ids[i : i + 16]).reshape(-1, V), labels[i : i + 16].reshape(-1),
+                                        reduction="sum").item()
+    loss_ref /= B * T
+    for name, q in ref_model.named_parameters():
+        ref_grads[name] = q.grad.detach().clone()
+    del ref_model
+    torch.cuda.empty_cache()
+
+    engine = fused.prepare_runtime(compute_dtype=torch.bfloat16)
+    engine.store.zero_grad()
+    loss = fused.fused_loss(ids, labels)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert abs(loss.item() - loss_ref) < 1e-2 * abs(loss_ref)
+    worst, worst_name = 0.0, ""
+    for name, p in fused.named_parameters():
+        q = ref_grads[name]
+        rel = ((p.grad.float() - q).norm() / (q.norm() + 1e-12)).item()
+        if rel > worst:
+            worst, worst_name = rel, name
+        assert rel < 3e-2, f"{name}: relative grad error {rel:.3e}"
+    print(f"worst relative grad error {worst:.3e} ({worst_name})")

@@ -71,7 +71,7 @@ def check() -> int:
     return 1 if bad else 0
 
 
-def time_shapes(model: str, M: int) -> None:
+def time_shapes(model: str, M: int, only: str = "") -> None:
     ops = _ops()
     for name, (N, K) in SHAPES[model].items():
         lda = 50304 if N == 50257 else N
@@ -89,20 +89,45 @@ def time_shapes(model: str, M: int) -> None:
             "pp_slab_bias": lambda: ops.wgrad_gemm_pp(dy, x, acc, bias, 0, 0),
         }
         for label, fn in variants.items():
+            if only and label not in only.split(","):
+                continue
             ms = timeit(fn)
             print(json.dumps({"model": model, "M": M, "gemm": name, "variant": label, "ms": round(ms, 4),
                               "TFLOPs": round(flops / ms / 1e9, 1)}), flush=True)
 
 
+def one(gemm: str, variant: str, M: int, reps: int) -> None:
+    """Run one shape / kernel ``reps`` times (a target for rocprofv3 counter passes)."""
+    ops = _ops()
+    N, K = {**SHAPES["gpt2-124m"], **SHAPES["head"]}[gemm]
+    lda = 50304 if N == 50257 else N
+    dy = torch.randn(M, lda, device="cuda", dtype=torch.bfloat16)[:, :N]
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    acc = torch.zeros(N, K, device="cuda")
+    fn = {"r3_tile256": lambda: ops.wgrad_gemm(dy, x, acc, 0, 256, 0),
+          "r3_pipe": lambda: ops.wgrad_gemm(dy, x, acc, 0, 256, 4),
+          "pp": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, -1)}[variant]
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["check", "time"])
+    ap.add_argument("what", choices=["check", "time", "one"])
+    ap.add_argument("--gemm", default="qkv")
+    ap.add_argument("--variant", default="pp")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--only", default="", help="comma-separated variant labels (time)")
     ap.add_argument("--tokens", type=int, default=131072)
     ap.add_argument("--model", default="gpt2-124m", choices=sorted(SHAPES))
     args = ap.parse_args()
     if args.what == "check":
         return check()
-    time_shapes(args.model, args.tokens)
+    if args.what == "one":
+        one(args.gemm, args.variant, args.tokens, args.reps)
+        return 0
+    time_shapes(args.model, args.tokens, args.only)
     return 0
 
 

@@ -416,7 +416,7 @@ def linear_dx_attn(dy, w, att, seqlen: int, v_bias_grad=None, head_dim: int = 64
 
 # Weight-gradient kernel: "pp" = the ping-pong kernel (csrc/gemm_wgrad_pp.hip: 8 waves, 2 per
 # SIMD, slab epilogue, bias column sums fused), "r3" = the round-3 kernels (csrc/gemm_wgrad.hip).
-WGRAD_KERNEL = os.environ.get("LLMTRAIN_WGRAD_KERNEL", "r3")
+WGRAD_KERNEL = os.environ.get("LLMTRAIN_WGRAD_KERNEL", "pp")
 
 
 def wgrad_fuses_bias() -> bool:

@@ -60,6 +60,40 @@ def test_flat_ddp_over_rccl_matches_single_process(nccl_world):
     assert diff <= 1e-3 * scale  # only float-atomic ordering differs
 
 
+def test_flat_ddp_rccl_bf16_buckets_stream_order_and_timeline(nccl_world):
+    """The RCCL branch of FlatDataParallel._launch with bf16 buckets: the comm stream casts, all-reduces
+    and copies back after the producing stream; the main stream's optimizer-side reader (after
+    finish_gradient_sync) sees the reduced bf16 values, and every bucket has ready / queue / comm
+    times from the three events."""
+    from llmtrain.parallel.reducer import FlatDataParallel
+
+    dev = nccl_world
+    torch.manual_seed(0)
+    base = GPT(vocab_size=512, block_size=128, d_model=256, n_layers=3, n_heads=4, d_ff=1024, dropout=0.0).to(dev)
+    solo = copy.deepcopy(base)
+    base.prepare_runtime(compute_dtype=torch.bfloat16)
+    solo.prepare_runtime(compute_dtype=torch.bfloat16)
+    ddp = FlatDataParallel(base, bucket_cap_mb=1.0, reduce_dtype=torch.bfloat16)
+    assert ddp._avg_native  # the RCCL path, not the gloo rehearsal
+    ids = torch.randint(0, 512, (4, 128), device=dev)
+    base.flat_store.zero_grad()
+    solo.flat_store.zero_grad()
+    ddp.fused_loss(ids, ids).backward()
+    ddp.finish_gradient_sync()
+    assert all(work is None for _, work, _ in ddp._works)  # waited on the comm stream, not the host
+    got = base.flat_store.grad.clone()  # main-stream reader, ordered after the comm stream
+    solo.fused_loss(ids, ids).backward()
+    torch.cuda.synchronize()
+    # every element went through the bf16 wire format (1 rank: AVG is the identity)
+    assert torch.equal(got, got.bfloat16().float())
+    ref = solo.flat_store.grad
+    assert (got - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+    steps = ddp.bucket_timeline()
+    assert len(steps) == 1 and len(steps[0]) == len(ddp.buckets)
+    for row in steps[0]:
+        assert row["queue_ms"] >= 0.0 and row["comm_ms"] >= 0.0 and row["ready_ms"] >= 0.0
+
+
 def test_trainer_metric_collectives_on_device(nccl_world, in_tmp):
     from llmtrain.config.schemas import RunConfig
     from llmtrain.parallel.dist import DDPState

@@ -3,9 +3,11 @@ synthetic token stream from the same seed through the fused bf16 engine and thro
 torch-module path (the reference numerics, models/gpt.py:109-184 + trainer.py:93-97, :390-393)
 must end at the same validation loss within a fixed relative bound.
 
-The bound (1 %) sits well above the bf16-vs-fp32 gaps measured at this shape (docs/parity.md) and
-well below what a broken kernel produces (a dropped dQ term or a wrong LayerNorm gradient moves the
-loss by tens of percent).  The statistic across seeds at GPT-2 124M is bench/parity.py --seeds."""
+The bound (0.1 %) is ten times the largest gap measured at this shape and these seeds (round 4:
+seed 1337 +0.0098 %, seed 7 +0.0005 %, profiles/r4/parity_gate_gaps.txt) and far below what a
+broken kernel produces (a dropped dQ term or a wrong LayerNorm gradient moves the loss by tens of
+percent; round 3's 1 % bound was ~100x the spread).  The statistic across seeds at GPT-2 124M is
+bench/parity.py --seeds (+0.002 % +- 0.011 % over 1,500 steps)."""
 
 from __future__ import annotations
 
@@ -16,7 +18,7 @@ from llmtrain.config.schemas import RunConfig
 
 pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("gpu_device")]
 
-BOUND = 0.01
+BOUND = 0.001
 
 
 def _cfg(fused: bool, seed: int) -> RunConfig:

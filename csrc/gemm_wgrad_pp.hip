@@ -44,6 +44,7 @@
 // (models/gpt.py:27-29, 94-96, 184 via loss.backward() at training/trainer.py:386-387).
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 
 #include "common.h"
 #include "gemm_common.h"
@@ -60,7 +61,7 @@ constexpr int TW = 256;        // tile edge
 constexpr int ROWB = TW * 2;   // LDS bytes per image row
 constexpr int IMG = BR * ROWB; // 16 KiB per operand per stage
 constexpr int SLOT = 2 * IMG;  // 32 KiB
-constexpr int NS = 4;          // ring slots
+constexpr int NS_MAX = 5;      // ring slots (4 or 5: template parameter NSL)
 constexpr int FA = 8, FB = 4;  // 16-wide fragments per wave: 128 (n) x 64 (k)
 constexpr int NACC = FA * FB;
 constexpr int SLAB_FLOATS = TW * TW;  // one tile's partial
@@ -78,7 +79,9 @@ __device__ __forceinline__ bf16x8 tr_read(unsigned addr) {
 
 // own LDS reads done and at most n (0, 2, 4, 6, 8) younger fill ops outstanding, then the barrier
 __device__ __forceinline__ void wait_fill_barrier(int n) {
-  if (n >= 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (n >= 12) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if (n >= 10) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else if (n >= 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else if (n >= 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else if (n >= 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -87,15 +90,36 @@ __device__ __forceinline__ void wait_fill_barrier(int n) {
 
 __device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
 
+// Buffer descriptor from provably wave-uniform inputs (readfirstlane of the base halves and the
+// record count): otherwise hipcc wraps every buffer load in a waterfall loop (playbook T20), which
+// also serialises them and drains vmcnt before each use.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, int bytes) {
+  const unsigned long a = (unsigned long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long)hi << 32) | lo), (short)0, n, 0x00020000);
+}
+
 // PLACE: where a wave issues its 4 fill ops of stage st+3 — 0: in LOAD(st) after its fragment
 // reads; 1: in MFMA(st), one after every 8 MFMAs; 2: the two A ops in LOAD(st), the two B ops in
 // MFMA(st).  (An LDS-DMA op costs its wave ~60 issue cycles among bare MFMAs but 100-185 inside a
 // phase that also reads fragments: MI355X_MICROARCH cycle constants.)
-template <int MODE, int PLACE>
+// SKEL (timing skeletons, never shipped, LLMT_WPP_SKEL): 1 = no fills inside the loop (every stage
+// re-reads the prologue's data); with LLMT_WPP_FILL=1 also 2 = global loads only (never written to
+// LDS), 3 = LDS writes of stale registers only (no loads) — to price each part of the fill.
+// FILL: 0 = LDS-DMA fills (PLACE / NSL as above); 1 = register-staged fills: each wave loads its
+// 4 x 16 bytes of stage st+3 into VGPRs (two register sets, stage parity) in LOAD(st) and writes
+// stage st+1's (loaded two phases earlier) to LDS with 16-byte lane-linear ds_write_b128 — the same
+// LDS image as the DMA fill.  Measured without fills the schedule runs 1.4-1.5 PF (LLMT_WPP_SKEL=1):
+// the LDS-DMA issue inside LOAD was what kept it at ~1.1.  With register staging a slot is free one
+// phase after its last read, so NSL = 2 (64 KiB) is legal as well as 4.
+template <int MODE, int PLACE, int NSL, int SKEL = 0, int FILL = 0>
 __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
     const bf16_raw* __restrict__ A, int lda, const bf16_raw* __restrict__ B, int ldb, float* __restrict__ C,
     int ldc, int M, int N, int K, int tiles, int tiles_k, int m_chunk, int split, int nwg, float* __restrict__ slab,
     float* __restrict__ bias_slab) {
+  constexpr int NS = NSL, D = NSL - 1;  // ring slots; stage st+D is filled while stage st is read
   __shared__ __attribute__((aligned(16))) bf16_raw smem[NS * SLOT / 2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -148,8 +172,11 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
   };
   // fill ops issued after stage st+1's last one at the wait in LOAD(st) (see PLACE)
   auto younger = [&](int st) {
-    const int s2 = st + 2 < nst ? 4 : 0, s3 = st + 3 < nst ? (PLACE == 0 ? 4 : PLACE == 2 ? 2 : 0) : 0;
-    return s2 + s3;
+    int n = 0;
+#pragma unroll
+    for (int s = 2; s < D; ++s) n += st + s < nst ? 4 : 0;  // whole stages issued in earlier phases
+    if (st + D < nst) n += PLACE == 0 ? 4 : PLACE == 2 ? 2 : 0;  // this LOAD's own ops
+    return n;
   };
 
   // fragment read addresses (bytes within a slot): lane (g, q, p) reads rows 8g + q (+4) at the
@@ -172,31 +199,76 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
   f32x4v bacc[2] = {0.f, 0.f};
   const bf16x8 ones = __builtin_bit_cast(bf16x8, (short8v){0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
 
-  // prologue: stages 0..2 in flight, stage 0 landed everywhere; Y then falls one barrier behind
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+  u32x4 R0[4], R1[4], R2[4];  // register-staged fills: FILL 1 stage parity (R0, R1); FILL 2 stage % 3
+  // (unconditional: a stage past the chunk has a zero-record descriptor and loads zeros — a
+  // conditional load made hipcc drain every outstanding load before each LDS write)
+  auto load_stage = [&](int st, u32x4 (&R)[4]) {
+    const int r0 = st * BR, nr = max(0, min(BR, rows - r0));
+    const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(A + (long)(m_begin + r0) * lda, nr * lda * 2);
+    const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(B + (long)(m_begin + r0) * ldb, nr * ldb * 2);
+    R[0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, voa[0], 0, 0));
+    R[1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, voa[1], 0, 0));
+    R[2] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, vob[0], 0, 0));
+    R[3] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, vob[1], 0, 0));
+  };
+  auto write_stage = [&](int slot, const u32x4 (&R)[4]) {
+    const unsigned a = lds + slot * SLOT + wave * 2048 + 16 * lane;
+    *(lds_u32x4*)(size_t)a = R[0];
+    *(lds_u32x4*)(size_t)(a + 1024) = R[1];
+    *(lds_u32x4*)(size_t)(a + IMG) = R[2];
+    *(lds_u32x4*)(size_t)(a + IMG + 1024) = R[3];
+  };
+
+  // prologue: stage 0 landed everywhere (DMA: stages 1..D-1 in flight; registers: stages 1 and 2
+  // loading); Y then falls one barrier behind
+  if (FILL == 0) {
 #pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (s < nst) fill(s, s);
-  wait_fill_barrier(4 * min(nst - 1, 2));
+    for (int s = 0; s < NS - 1; ++s)
+      if (s < nst) fill(s, s);
+    wait_fill_barrier(4 * min(nst - 1, D - 1));
+  } else {
+    load_stage(0, R0);
+    load_stage(1, R1);
+    if (FILL == 2) load_stage(2, R2);
+    write_stage(0, R0);
+    load_stage(FILL == 2 ? 3 : 2, R0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
   if (wn == 1) barrier();
 
-  auto phase = [&](int st, int slot) {
+  // R: the register set of stage st+1 (= that of st+3)
+  auto phase = [&](int st, int slot, u32x4 (&R)[4]) {
     // ---- LOAD(st): fragments of stage st, fill of stage st+3 into the slot of stage st-1
     const unsigned sb = lds + slot * SLOT;
-    const bool refill = st + 3 < nst;
-    const int fslot = (slot + 3) & 3;
+    const bool refill = FILL == 0 && SKEL == 0 && st + D < nst;
+    const int fslot = slot == 0 ? NS - 1 : slot - 1;  // the slot of stage st-1 = that of st+D
     bf16x8 af[FA], bfr[FB];
 #pragma unroll
     for (int i = 0; i < FA; ++i) af[i] = tr_read(sb + ao[i]);
 #pragma unroll
     for (int j = 0; j < FB; ++j) bfr[j] = tr_read(sb + bo[j]);
     if (refill) {
-      if (PLACE == 0) fill(st + 3, fslot);
+      if (PLACE == 0) fill(st + D, fslot);
       if (PLACE == 2) {
-        fill_op(st + 3, fslot, 0);
-        fill_op(st + 3, fslot, 1);
+        fill_op(st + D, fslot, 0);
+        fill_op(st + D, fslot, 1);
       }
     }
-    wait_fill_barrier(younger(st));
+    if (FILL == 0) {
+      wait_fill_barrier(younger(st));
+    } else {
+      // stage st+1 (loaded two phases ago) into its slot, stage st+3 into the freed registers; both
+      // unconditional (a slot past the last stage is never read)
+      if (SKEL == 0 || SKEL == 3) write_stage(slot + 1 == NS ? 0 : slot + 1, R);  // 3: stale data
+      if (SKEL == 0 || SKEL == 2) load_stage(st + (FILL == 2 ? 4 : 3), R);
+      if (SKEL == 2) {  // loads kept live, never written to LDS
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(R[j]));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
     // ---- MFMA(st)
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
@@ -208,7 +280,7 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
       // it before the barrier that opened this segment)
       if ((PLACE == 1 && (i & 1)) || (PLACE == 2 && (i == 3 || i == 7))) {
         __builtin_amdgcn_sched_barrier(0);
-        if (refill) fill_op(st + 3, fslot, PLACE == 1 ? i >> 1 : (i == 3 ? 2 : 3));
+        if (refill) fill_op(st + D, fslot, PLACE == 1 ? i >> 1 : (i == 3 ? 2 : 3));
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -220,11 +292,40 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
     __builtin_amdgcn_sched_barrier(0);
     barrier();
   };
-  for (int s0 = 0; s0 < nst; s0 += NS) {
-    phase(s0, 0);
-    if (s0 + 1 < nst) phase(s0 + 1, 1);
-    if (s0 + 2 < nst) phase(s0 + 2, 2);
-    if (s0 + 3 < nst) phase(s0 + 3, 3);
+  if (NS == 5) {
+    for (int s0 = 0; s0 < nst; s0 += 5) {  // (DMA only; registers unused)
+      phase(s0, 0, R1);
+      if (s0 + 1 < nst) phase(s0 + 1, 1, R0);
+      if (s0 + 2 < nst) phase(s0 + 2, 2, R1);
+      if (s0 + 3 < nst) phase(s0 + 3, 3, R0);
+      if (s0 + 4 < nst) phase(s0 + 4, 4, R1);
+    }
+  } else if (FILL == 2) {
+    // three register sets: a stage's loads get three phases (not two) to land before its LDS write;
+    // groups of 6 unconditional phases (2 slots x 3 sets), zero stages past the chunk
+    for (int s0 = 0; s0 < nst; s0 += 6) {
+      phase(s0, 0, R1);
+      phase(s0 + 1, 1, R2);
+      phase(s0 + 2, 0, R0);
+      phase(s0 + 3, 1, R1);
+      phase(s0 + 4, 0, R2);
+      phase(s0 + 5, 1, R0);
+    }
+  } else if (FILL == 1 && NS == 2) {
+    // register-staged, 2 slots: pairs of phases with no per-phase condition (a conditional phase
+    // made hipcc assume the loads of a skipped phase were never issued and drain vmcnt early); an
+    // odd last stage is padded with a stage of zeros (zero-record loads, MFMAs on zeros)
+    for (int s0 = 0; s0 < nst; s0 += 2) {
+      phase(s0, 0, R1);
+      phase(s0 + 1, 1, R0);
+    }
+  } else {
+    for (int s0 = 0; s0 < nst; s0 += 4) {  // stage parity and slot are compile-time in each step
+      phase(s0, 0, R1);
+      if (s0 + 1 < nst) phase(s0 + 1, 1 % NS, R0);
+      if (s0 + 2 < nst) phase(s0 + 2, 2 % NS, R1);
+      if (s0 + 3 < nst) phase(s0 + 3, 3 % NS, R0);
+    }
   }
   if (wn == 0) barrier();  // X matches Y's extra barrier
 
@@ -238,7 +339,11 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
       const int r = lane & 3;
       const float v = r == 0 ? bacc[t][0] : r == 1 ? bacc[t][1] : r == 2 ? bacc[t][2] : bacc[t][3];
       const int n = n0 + 128 * wn + 16 * (2 * wk + t) + 4 * g + r;
-      if ((lane & 15) < 4 && n < N) bias_slab[(long)chunk * N + n] = v;
+      // atomic epilogue (fast mode): straight into the bias vector; otherwise this chunk's row
+      if ((lane & 15) < 4 && n < N) {
+        if (MODE == 2) atomicAdd(bias_slab + n, v);
+        else bias_slab[(long)chunk * N + n] = v;
+      }
     }
   }
   if (MODE == 0) {
@@ -357,6 +462,13 @@ PPPlan plan_pp(int M, int N, int K, int split_req, int mode_req, int ncu, int mi
 }
 
 hipError_t plan_wgrad_pp(int lda, int ldb, int M, int N, int K, int split, int mode, bool det, PPPlan& p) {
+  // LLMT_WPP_EPI=atomic|slab: the auto plan's split-K epilogue in fast mode (A/B knob)
+  static const int epi = [] {
+    const char* e = std::getenv("LLMT_WPP_EPI");
+    if (e == nullptr) return -1;
+    return std::string(e) == "atomic" ? 2 : std::string(e) == "slab" ? 0 : -1;
+  }();
+  if (mode < 0) mode = epi;
   if (lda % 8 || ldb % 8 || K % 8 || lda < N) return hipErrorInvalidValue;
   // one stage of either operand must stay below the 32-bit buffer range
   if ((long long)wpp::BR * std::max(lda, ldb) * 2 >= (1LL << 31)) return hipErrorInvalidValue;
@@ -371,7 +483,7 @@ long wgrad_pp_ws_floats(int lda, int ldb, int M, int N, int K, int split, int mo
   PPPlan p;
   if (plan_wgrad_pp(lda, ldb, M, N, K, split, mode, deterministic(), p) != hipSuccess) return 0;
   long f = p.mode == 0 && p.split > 1 ? (long)p.tiles * p.split * wpp::SLAB_FLOATS : 0;
-  if (bias) f += (long)p.split * N;
+  if (bias && !(p.mode == 2 && p.split > 1)) f += (long)p.split * N;
   return f;
 }
 
@@ -383,29 +495,85 @@ hipError_t launch_wgrad_pp(const void* dy, int lda, const void* x, int ldb, floa
   if (e != hipSuccess) return e;
   const int nwg = p.tiles * p.split;
   const bool slabs = p.mode == 0 && p.split > 1;
+  const bool atomic = !slabs && p.split > 1;  // mode 2: partials and bias sums added with fp32 atomics
   float* slab = slabs ? ws : nullptr;
-  float* bias_parts = bias != nullptr ? ws + (slabs ? (long)p.tiles * p.split * wpp::SLAB_FLOATS : 0) : nullptr;
-  if ((slabs || bias != nullptr) && ws == nullptr) return hipErrorInvalidValue;
+  float* bias_parts =
+      bias == nullptr ? nullptr : atomic ? bias : ws + (slabs ? (long)p.tiles * p.split * wpp::SLAB_FLOATS : 0);
+  if ((slabs || (bias != nullptr && !atomic)) && ws == nullptr) return hipErrorInvalidValue;
   const int m = slabs ? 0 : (p.split == 1 ? 1 : 2);
+  // A/B knobs of the schedule (docs/round4.md): LLMT_WPP_PLACE (fill-op placement, 0 / 2),
+  // LLMT_WPP_SLOTS (4 or 5 ring slots = 128 / 160 KiB of LDS)
   static const int place = [] {
     const char* e = std::getenv("LLMT_WPP_PLACE");
     return e != nullptr ? std::atoi(e) : 0;
   }();
-#define LLMT_PP_LAUNCH(MD, PL)                                                                                      \
-  hipLaunchKernelGGL((wpp::wgrad_pp_kernel<MD, PL>), dim3(nwg), dim3(wpp::kThreads), 0, stream, (const bf16_raw*)dy, \
-                     lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k, p.m_chunk, p.split, nwg,     \
-                     slab, bias_parts)
-#define LLMT_PP_MODES(PL)         \
-  if (m == 0) LLMT_PP_LAUNCH(0, PL); \
-  else if (m == 1) LLMT_PP_LAUNCH(1, PL); \
-  else LLMT_PP_LAUNCH(2, PL);
-  if (place == 1) { LLMT_PP_MODES(1) }
-  else if (place == 2) { LLMT_PP_MODES(2) }
-  else { LLMT_PP_MODES(0) }
+  static const int skel = [] {
+    const char* e = std::getenv("LLMT_WPP_SKEL");
+    return e != nullptr ? std::atoi(e) : 0;
+  }();
+  // default: register-staged fills through a 2-slot (64 KiB) ring (op level +2-4 % over LDS-DMA
+  // on one box, a tie on another; step +0.5 % at mb 128: profiles/r4/wgrad/ab_fill_mb*.txt) —
+  // half the LDS leaves room for main-stream workgroups on the same CU
+  static const int fillmode = [] {
+    const char* e = std::getenv("LLMT_WPP_FILL");
+    return e != nullptr ? std::atoi(e) : 1;
+  }();
+  static const int slots = [] {
+    const char* e = std::getenv("LLMT_WPP_SLOTS");
+    const int v = e != nullptr ? std::atoi(e) : (fillmode == 1 ? 2 : 4);
+    return v == 5 || v == 2 ? v : 4;
+  }();
+#define LLMT_PP_LAUNCH(MD, PL, NSL)                                                                             \
+  hipLaunchKernelGGL((wpp::wgrad_pp_kernel<MD, PL, NSL>), dim3(nwg), dim3(wpp::kThreads), 0, stream,             \
+                     (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k,     \
+                     p.m_chunk, p.split, nwg, slab, bias_parts)
+#define LLMT_PP_MODES(PL, NSL)                \
+  if (m == 0) LLMT_PP_LAUNCH(0, PL, NSL);      \
+  else if (m == 1) LLMT_PP_LAUNCH(1, PL, NSL); \
+  else LLMT_PP_LAUNCH(2, PL, NSL);
+#define LLMT_RS_LAUNCH(MD, NSL, SK)                                                                       \
+  hipLaunchKernelGGL((wpp::wgrad_pp_kernel<MD, 0, NSL, SK, 1>), dim3(nwg), dim3(wpp::kThreads), 0, stream,  \
+                     (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k, \
+                     p.m_chunk, p.split, nwg, slab, bias_parts)
+  if (fillmode == 2) {
+    if (m == 0) hipLaunchKernelGGL((wpp::wgrad_pp_kernel<0, 0, 2, 0, 2>), dim3(nwg), dim3(wpp::kThreads), 0, stream,
+                                   (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles,
+                                   p.tiles_k, p.m_chunk, p.split, nwg, slab, bias_parts);
+    else if (m == 1) hipLaunchKernelGGL((wpp::wgrad_pp_kernel<1, 0, 2, 0, 2>), dim3(nwg), dim3(wpp::kThreads), 0,
+                                        stream, (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K,
+                                        p.tiles, p.tiles_k, p.m_chunk, p.split, nwg, slab, bias_parts);
+    else hipLaunchKernelGGL((wpp::wgrad_pp_kernel<2, 0, 2, 0, 2>), dim3(nwg), dim3(wpp::kThreads), 0, stream,
+                            (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k,
+                            p.m_chunk, p.split, nwg, slab, bias_parts);
+  } else if (fillmode == 1) {
+    if (skel == 1) LLMT_RS_LAUNCH(0, 4, 1);
+    else if (skel == 2) LLMT_RS_LAUNCH(0, 2, 2);
+    else if (skel == 3) LLMT_RS_LAUNCH(0, 2, 3);
+    else if (slots == 2) {
+      if (m == 0) LLMT_RS_LAUNCH(0, 2, 0);
+      else if (m == 1) LLMT_RS_LAUNCH(1, 2, 0);
+      else LLMT_RS_LAUNCH(2, 2, 0);
+    } else {
+      if (m == 0) LLMT_RS_LAUNCH(0, 4, 0);
+      else if (m == 1) LLMT_RS_LAUNCH(1, 4, 0);
+      else LLMT_RS_LAUNCH(2, 4, 0);
+    }
+  } else if (skel == 1) {
+    hipLaunchKernelGGL((wpp::wgrad_pp_kernel<0, 0, 4, 1>), dim3(nwg), dim3(wpp::kThreads), 0, stream,
+                       (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k,
+                       p.m_chunk, p.split, nwg, slab, bias_parts);
+  } else if (slots == 5) {
+    if (place == 2) { LLMT_PP_MODES(2, 5) }
+    else { LLMT_PP_MODES(0, 5) }
+  } else {
+    if (place == 2) { LLMT_PP_MODES(2, 4) }
+    else { LLMT_PP_MODES(0, 4) }
+  }
 #undef LLMT_PP_MODES
 #undef LLMT_PP_LAUNCH
+#undef LLMT_RS_LAUNCH
   const long total = slabs ? (long)p.tiles * 8 * wpp::NACC * 64 : 0;
-  const int nbias = bias != nullptr ? N : 0;
+  const int nbias = bias != nullptr && !atomic ? N : 0;
   if (total + nbias > 0)
     hipLaunchKernelGGL(wpp::wgrad_finish_kernel, dim3((unsigned)((total + nbias + 255) / 256)), dim3(256), 0, stream,
                        slab, p.split, c, ldc, N, K, p.tiles_k, total, bias_parts, bias, nbias);

@@ -1,0 +1,13 @@
+# weight-gradient ping-pong kernel: full vs no-fill timing skeleton (LLMT_WPP_SKEL=1)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out/s6
+for rnd in 1 2; do
+for sk in 0 1; do
+  LLMT_WPP_SKEL=$sk timeout -k 10 120 python -u bench/wgrad_pp.py time --tokens 131072 --only pp_slab,pp_slab_bias > gpurun_out/s6/skel${sk}_r$rnd.log 2>&1 || exit 1
+done
+done
+for f in gpurun_out/s6/skel*.log; do echo "$f"; grep -v amdgpu "$f" | python3 -c "
+import sys,json
+for l in sys.stdin:
+    d=json.loads(l); print('  ', d['gemm'], d['variant'], d['ms'], d['TFLOPs'])"; done

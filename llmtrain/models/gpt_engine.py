@@ -188,9 +188,13 @@ class FusedGPTEngine:
         # per-forward dropout base seed provider (None: one draw from torch's CPU generator)
         self.drop_seed_source: Callable[[], int] | None = None
         self._anchor = torch.zeros((), requires_grad=True, device=self.store.device)
-        # weight-gradient GEMMs on a second HIP stream, overlapping the dX GEMMs and the
-        # bandwidth-bound backward kernels of the main stream (LLMTRAIN_WGRAD_STREAM=0 disables)
-        self.wgrad_stream_enabled = os.environ.get("LLMTRAIN_WGRAD_STREAM", "1") != "0"
+        # weight-gradient GEMMs on a second HIP stream beside the main stream's dX GEMMs and
+        # bandwidth-bound kernels (LLMTRAIN_WGRAD_STREAM=1).  Off by default since round 4: the
+        # ping-pong weight-gradient kernel takes 2 x 236 registers of every SIMD it lands on, so
+        # nothing of the main stream co-resides with it and the two streams only time-share the
+        # chip; one stream measured +0.9 % at micro-batch 128 and +1.0 % at 32 (same box,
+        # profiles/r4/ab_side_stream_vs_one_stream_mb*.txt), and is the deterministic schedule.
+        self.wgrad_stream_enabled = os.environ.get("LLMTRAIN_WGRAD_STREAM", "0") != "0"
         # hand-written MFMA GEMM (csrc/gemm_fused.hip) where it beats hipBLASLt: qkv and attention
         # output projections (forward and dX), the fc forward with bias + GELU in its epilogue, the
         # MLP projection dX with the GELU backward + fc-bias gradient in its epilogue

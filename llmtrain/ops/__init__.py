@@ -267,7 +267,7 @@ FGEMM_MAX_A_BYTES = 64 * 2**20
 # stores at this size, fc + bias + GELU on ours beats hipBLASLt + the GELU pass alone (0.725 vs
 # 0.808 ms) but runs 0.86 ms per call inside the step and the step loses 0.4-1.0 % (qkv forward
 # too: -1.2 %; profiles/r3/nt/), so those stay on hipBLASLt.
-FGEMM_ANY_SIZE = frozenset({"dx_gelu", "dx_attn"})
+FGEMM_ANY_SIZE = frozenset(os.environ.get("LLMTRAIN_FGEMM_ANY", "dx_gelu,dx_attn").split(","))  # A/B knob
 
 
 _WARNED: set[str] = set()

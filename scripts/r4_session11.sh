@@ -8,3 +8,6 @@ LLMT_WPP_EPI=atomic timeout -k 10 120 python -u bench/wgrad_pp.py time --tokens 
 bash scripts/abn.sh "LLMT_WPP_EPI=slab" "LLMT_WPP_EPI=atomic" -- --steps 20 --warmup 5 > gpurun_out/s11/ab_epi_mb128.txt 2>&1 || exit 1
 bash scripts/abn.sh "LLMT_WPP_EPI=slab" "LLMT_WPP_EPI=atomic" -- --steps 30 --warmup 5 --micro-batch 32 > gpurun_out/s11/ab_epi_mb32.txt 2>&1 || exit 1
 cat gpurun_out/s11/ab_epi_mb128.txt gpurun_out/s11/ab_epi_mb32.txt
+bash scripts/abn.sh "LLMTRAIN_DET_SCHEDULE=serial" "LLMTRAIN_DET_SCHEDULE=ours" -- --steps 20 --warmup 5 --deterministic > gpurun_out/s11/ab_det_mb128.txt 2>&1 || exit 1
+bash scripts/abn.sh "LLMTRAIN_DET_SCHEDULE=serial" "LLMTRAIN_DET_SCHEDULE=ours" -- --steps 30 --warmup 5 --micro-batch 32 --deterministic > gpurun_out/s11/ab_det_mb32.txt 2>&1 || exit 1
+cat gpurun_out/s11/ab_det_mb128.txt gpurun_out/s11/ab_det_mb32.txt

@@ -122,7 +122,9 @@ def test_trainer_metric_collectives_on_device(nccl_world, in_tmp):
 
 
 def _two_rank_worker(rank: int, world: int, port: int, out_dir: str) -> None:
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    # the side-stream schedule (opt-in since round 4) keeps its reducer coverage here
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
+                      LLMTRAIN_WGRAD_STREAM="1")
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from llmtrain.parallel.reducer import FlatDataParallel

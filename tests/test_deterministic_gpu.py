@@ -155,18 +155,22 @@ def _det_cfg():
     })
 
 
-def test_deterministic_training_runs_are_bitwise_equal() -> None:
-    """run.deterministic with the DEFAULT engine (weight-gradient side stream on): two 50-step GPT-2
-    124M runs in one process, issued exactly like Trainer.fit (no host sync between steps), end with
-    bitwise-equal master weights and agree at every step.  Before every GEMM moved onto the
-    hand-written kernels in this mode, the first run of a process diverged from later ones
-    (hipBLASLt Stream-K beside the side stream; bench/determinism_probe.py --runs, docs/round3.md)."""
+@pytest.mark.parametrize("schedule", ["serial", "ours"])
+def test_deterministic_training_runs_are_bitwise_equal(schedule: str, monkeypatch: pytest.MonkeyPatch) -> None:
+    """run.deterministic: two 50-step GPT-2 124M runs in one process, issued exactly like
+    Trainer.fit (no host sync between steps), end with bitwise-equal master weights and agree at
+    every step — for the default "serial" schedule (one stream, hipBLASLt forward / dX GEMMs) and the
+    "ours" schedule (weight-gradient side stream on, every GEMM on the hand-written kernels).  Round 3
+    found the first run of a process diverging with hipBLASLt's Stream-K GEMMs BESIDE the side
+    stream (bench/determinism_probe.py --runs, docs/round3.md); neither schedule has that pairing."""
     from llmtrain.training.trainer import Trainer
 
+    monkeypatch.setenv("LLMTRAIN_DET_SCHEDULE", schedule)
+    monkeypatch.setenv("LLMTRAIN_WGRAD_STREAM", "1" if schedule == "ours" else "0")
     outs = []
     for _ in range(2):
         trainer = Trainer(_det_cfg())
-        assert trainer.model.engine.wgrad_stream_enabled
+        assert trainer.model.engine._side_stream() is (None if schedule == "serial" else trainer.model.engine._side)
         stream = trainer.batch_stream()
         losses = [trainer.train_step(stream)[0].reshape(1) for _ in range(50)]
         torch.cuda.synchronize()

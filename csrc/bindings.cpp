@@ -530,6 +530,15 @@ void wgrad_gemm_pp(const Tensor& dy, const Tensor& x, Tensor c, const c10::optio
             "wgrad_gemm_pp");
 }
 
+// timing probe of the ping-pong kernel (LLMT_WPP_SKEL=9): buf = int64 [256 * 8 * 8]
+// (an empty tensor clears it)
+void wgrad_pp_probe(const Tensor& buf) {
+  check_gpu(buf, "buf");
+  TORCH_CHECK(buf.numel() == 0 || (buf.scalar_type() == at::kLong && buf.numel() >= 256 * 64),
+              "wgrad_pp_probe: int64[16384]");
+  check_hip(llmt::wgrad_pp_set_probe(buf.numel() ? buf.data_ptr() : nullptr), "wgrad_pp_probe");
+}
+
 // ---- fused forward / dX GEMM ------------------------------------------------------------------
 // out = epi(a @ op(b)): b is [N, K] (weight, forward) or, with b_kn, [K, N] (weight in dX = dy @ W).
 // epilogue 0 -> (out, None); 1 -> (u, gelu(u)); 2 -> (du = acc * gelu'(u), None) with dbias += colsum.
@@ -711,6 +720,7 @@ TORCH_LIBRARY(llmtrain_hip, m) {
   m.def("get_deterministic() -> bool", &get_deterministic);
   m.def("set_dropout_seed_offset(Tensor? word) -> ()", &set_dropout_seed_offset);
   m.def("wgrad_gemm(Tensor dy, Tensor x, Tensor(a!) c, int split=0, int tile=0, int pipe=-1) -> ()");
+  m.def("wgrad_pp_probe(Tensor buf) -> ()");
   m.def("wgrad_gemm_pp(Tensor dy, Tensor x, Tensor(a!) c, Tensor(b!)? bias=None, int split=0, int mode=-1) -> ()");
   m.def("gemm_fused(Tensor a, Tensor b, bool b_kn, int epilogue, Tensor? bias=None, Tensor? u=None,"
         " Tensor(a!)? dbias=None, int seq_len=0) -> (Tensor, Tensor?)");
@@ -739,6 +749,7 @@ TORCH_LIBRARY_IMPL(llmtrain_hip, CUDA, m) {
   m.impl("dropout_mask", &dropout_mask);
   m.impl("wgrad_gemm", &wgrad_gemm);
   m.impl("wgrad_gemm_pp", &wgrad_gemm_pp);
+  m.impl("wgrad_pp_probe", &wgrad_pp_probe);
   m.impl("gemm_fused", &gemm_fused);
   m.impl("sumsq", &sumsq);
   m.impl("adamw_flat", &adamw_flat);

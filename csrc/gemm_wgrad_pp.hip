@@ -68,6 +68,11 @@ constexpr int SLAB_FLOATS = TW * TW;  // one tile's partial
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
+// Timing probe (SKEL 9, LLMT_WPP_SKEL=9, bench/wgrad_pp.py probe): per wave, the shader-clock
+// cycles spent in each part of a phase summed over the phases, stored by workgroups < 256
+// as probe[(wg * 8 + wave) * 8 + part]
+__device__ unsigned long long* g_wpp_probe = nullptr;
+
 __device__ __forceinline__ int swz_f(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
 
 __device__ __forceinline__ bf16x8 tr_read(unsigned addr) {
@@ -228,6 +233,17 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
     for (int s = 0; s < NS - 1; ++s)
       if (s < nst) fill(s, s);
     wait_fill_barrier(4 * min(nst - 1, D - 1));
+  } else if (FILL == 3) {
+    // X keeps stage s in set s & 1, Y in set (s + 1) & 1, so both use set (st + 1) & 1 in phase st:
+    // X writes stages 0 (and 1, rewritten in MFMA(0)), Y stages 0 and 1; then X loads 1, 2 and
+    // Y loads 2, 3 (older load first: the set written next is the one that must have landed)
+    load_stage(wn, R0);
+    load_stage(1 - wn, R1);
+    write_stage(wn, R0);
+    write_stage(1 - wn, R1);
+    load_stage(1 + wn, R1);
+    load_stage(2 + wn, R0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   } else {
     load_stage(0, R0);
     load_stage(1, R1);
@@ -238,10 +254,17 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
   }
   if (wn == 1) barrier();
 
+  unsigned long long pr[6] = {0, 0, 0, 0, 0, 0}, pt2 = 0, pt3 = 0, pt4 = 0, pt5 = 0;
   // R: the register set of stage st+1 (= that of st+3)
   auto phase = [&](int st, int slot, u32x4 (&R)[4]) {
     // ---- LOAD(st): fragments of stage st, fill of stage st+3 into the slot of stage st-1
     const unsigned sb = lds + slot * SLOT;
+    unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+    if (SKEL == 9) {
+      __builtin_amdgcn_sched_barrier(0);
+      t0 = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+    }
     const bool refill = FILL == 0 && SKEL == 0 && st + D < nst;
     const int fslot = slot == 0 ? NS - 1 : slot - 1;  // the slot of stage st-1 = that of st+D
     bf16x8 af[FA], bfr[FB];
@@ -249,6 +272,11 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
     for (int i = 0; i < FA; ++i) af[i] = tr_read(sb + ao[i]);
 #pragma unroll
     for (int j = 0; j < FB; ++j) bfr[j] = tr_read(sb + bo[j]);
+    if (SKEL == 9) {
+      __builtin_amdgcn_sched_barrier(0);
+      t1 = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if (refill) {
       if (PLACE == 0) fill(st + D, fslot);
       if (PLACE == 2) {
@@ -258,11 +286,19 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
     }
     if (FILL == 0) {
       wait_fill_barrier(younger(st));
+    } else if (FILL == 3) {
+      if (SKEL == 9) t2 = t1;
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     } else {
       // stage st+1 (loaded two phases ago) into its slot, stage st+3 into the freed registers; both
       // unconditional (a slot past the last stage is never read)
-      if (SKEL == 0 || SKEL == 3) write_stage(slot + 1 == NS ? 0 : slot + 1, R);  // 3: stale data
-      if (SKEL == 0 || SKEL == 2) load_stage(st + (FILL == 2 ? 4 : 3), R);
+      if (SKEL == 0 || SKEL == 3 || SKEL == 9) write_stage(slot + 1 == NS ? 0 : slot + 1, R);  // 3: stale data
+      if (SKEL == 0 || SKEL == 2 || SKEL == 9) load_stage(st + (FILL == 2 ? 4 : 3), R);
+      if (SKEL == 9) {
+        __builtin_amdgcn_sched_barrier(0);
+        t2 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+      }
       if (SKEL == 2) {  // loads kept live, never written to LDS
 #pragma unroll
         for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(R[j]));
@@ -271,16 +307,64 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
     }
     // ---- MFMA(st)
     __builtin_amdgcn_sched_barrier(0);
+    if (SKEL == 9) {
+      // every stamp issued so far has returned (lgkmcnt(0) above): account them here, where the
+      // compiler's own wait costs nothing; this phase's t3..t5 are accounted one phase later
+      pr[0] += t1 - t0;  // fragment reads issued
+      pr[1] += t2 - t1;  // LDS writes + global loads issued
+      if (pt2 != 0) {
+        pr[2] += pt3 - pt2;  // wait for own LDS ops + barrier A (+ first MFMA)
+        pr[3] += pt4 - pt3;  // remaining MFMA issue
+        pr[4] += pt5 - pt4;  // barrier B
+        pr[5] += 1;
+      }
+      pt2 = t2;
+      __builtin_amdgcn_sched_barrier(0);
+    }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < FA; ++i) {
 #pragma unroll
-      for (int j = 0; j < FB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < FB; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        if (SKEL == 9 && i == 0 && j == 0) {  // after the compiler's fragment wait
+          __builtin_amdgcn_sched_barrier(0);
+          t3 = __builtin_amdgcn_s_memtime();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
       // fill ops between MFMA groups (the slot of stage st-1 is free: every wave finished reading
       // it before the barrier that opened this segment)
-      if ((PLACE == 1 && (i & 1)) || (PLACE == 2 && (i == 3 || i == 7))) {
+      if (FILL == 0 && ((PLACE == 1 && (i & 1)) || (PLACE == 2 && (i == 3 || i == 7)))) {
         __builtin_amdgcn_sched_barrier(0);
         if (refill) fill_op(st + D, fslot, PLACE == 1 ? i >> 1 : (i == 3 ? 2 : 3));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // FILL 3: the fill rides in this wave's own MFMA segment.  X writes stage st+1 into the slot
+      // of stage st-1 (Y's last reads of it ended a barrier before this segment opened) and loads
+      // stage st+3; Y, one barrier later, writes stage st+2 into the slot of stage st (every wave
+      // finished reading it at the barrier that opened this segment) and loads stage st+4; each
+      // group's writes land before the barrier closing the segment, ahead of the first reader.
+      // Parts: A-row writes, B-row writes, A loads, B loads.
+      const int part = PLACE == 1 ? ((i & 1) ? i >> 1 : -1) : (i < 4 ? i : -1);
+      if (FILL == 3 && part >= 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (part < 2) {
+          const unsigned a = lds + ((st + 1 - wn) & 1) * SLOT + wave * 2048 + 16 * lane + part * IMG;
+          *(lds_u32x4*)(size_t)a = R[2 * part];
+          *(lds_u32x4*)(size_t)(a + 1024) = R[2 * part + 1];
+        } else {
+          const int ls = st + 3 + wn, r0 = ls * BR, nr = max(0, min(BR, rows - r0));
+          if (part == 2) {
+            const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(A + (long)(m_begin + r0) * lda, nr * lda * 2);
+            R[0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, voa[0], 0, 0));
+            R[1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, voa[1], 0, 0));
+          } else {
+            const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(B + (long)(m_begin + r0) * ldb, nr * ldb * 2);
+            R[2] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, vob[0], 0, 0));
+            R[3] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, vob[1], 0, 0));
+          }
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -290,7 +374,19 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
     }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
-    barrier();
+    if (SKEL == 9) {
+      t4 = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (FILL == 3) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // own writes landed
+    else barrier();
+    if (SKEL == 9) {
+      __builtin_amdgcn_sched_barrier(0);
+      pt5 = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+      pt3 = t3;
+      pt4 = t4;
+    }
   };
   if (NS == 5) {
     for (int s0 = 0; s0 < nst; s0 += 5) {  // (DMA only; registers unused)
@@ -311,7 +407,7 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
       phase(s0 + 4, 0, R2);
       phase(s0 + 5, 1, R0);
     }
-  } else if (FILL == 1 && NS == 2) {
+  } else if ((FILL == 1 || FILL == 3) && NS == 2) {
     // register-staged, 2 slots: pairs of phases with no per-phase condition (a conditional phase
     // made hipcc assume the loads of a skipped phase were never issued and drain vmcnt early); an
     // odd last stage is padded with a stage of zeros (zero-record loads, MFMAs on zeros)
@@ -328,6 +424,16 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
     }
   }
   if (wn == 0) barrier();  // X matches Y's extra barrier
+  if (SKEL == 9) {  // the last phase
+    pr[2] += pt3 - pt2;
+    pr[3] += pt4 - pt3;
+    pr[4] += pt5 - pt4;
+    pr[5] += 1;
+  }
+  if (SKEL == 9 && g_wpp_probe != nullptr && blockIdx.x < 256 && lane == 0) {
+#pragma unroll
+    for (int e = 0; e < 6; ++e) g_wpp_probe[(blockIdx.x * 8 + wave) * 8 + e] = pr[e];
+  }
 
   // ---- epilogue.  Accumulator (i, j) register r of lane l: n = n0 + 128 wn + 16 ((i + 2wk) & 7)
   // + 4 (l >> 4) + r, k = k0 + 64 wk + 16 j + (l & 15)
@@ -478,6 +584,11 @@ hipError_t plan_wgrad_pp(int lda, int ldb, int M, int N, int K, int split, int m
 }
 }  // namespace
 
+hipError_t wgrad_pp_set_probe(void* buf) {
+  unsigned long long* p = (unsigned long long*)buf;
+  return hipMemcpyToSymbol(HIP_SYMBOL(wpp::g_wpp_probe), &p, sizeof(p));
+}
+
 long wgrad_pp_ws_floats(int lda, int ldb, int M, int N, int K, int split, int mode, bool bias) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   PPPlan p;
@@ -520,7 +631,7 @@ hipError_t launch_wgrad_pp(const void* dy, int lda, const void* x, int ldb, floa
   }();
   static const int slots = [] {
     const char* e = std::getenv("LLMT_WPP_SLOTS");
-    const int v = e != nullptr ? std::atoi(e) : (fillmode == 1 ? 2 : 4);
+    const int v = e != nullptr ? std::atoi(e) : (fillmode == 1 || fillmode == 3 ? 2 : 4);
     return v == 5 || v == 2 ? v : 4;
   }();
 #define LLMT_PP_LAUNCH(MD, PL, NSL)                                                                             \
@@ -545,8 +656,27 @@ hipError_t launch_wgrad_pp(const void* dy, int lda, const void* x, int ldb, floa
     else hipLaunchKernelGGL((wpp::wgrad_pp_kernel<2, 0, 2, 0, 2>), dim3(nwg), dim3(wpp::kThreads), 0, stream,
                             (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k,
                             p.m_chunk, p.split, nwg, slab, bias_parts);
+  } else if (fillmode == 3) {
+#define LLMT_RS3_LAUNCH(MD, PL, SK)                                                                        \
+  hipLaunchKernelGGL((wpp::wgrad_pp_kernel<MD, PL, 2, SK, 3>), dim3(nwg), dim3(wpp::kThreads), 0, stream,    \
+                     (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k, \
+                     p.m_chunk, p.split, nwg, slab, bias_parts)
+    if (skel == 9 && m == 0) {
+      if (place == 1) LLMT_RS3_LAUNCH(0, 1, 9);
+      else LLMT_RS3_LAUNCH(0, 0, 9);
+    } else if (place == 1) {
+      if (m == 0) LLMT_RS3_LAUNCH(0, 1, 0);
+      else if (m == 1) LLMT_RS3_LAUNCH(1, 1, 0);
+      else LLMT_RS3_LAUNCH(2, 1, 0);
+    } else {
+      if (m == 0) LLMT_RS3_LAUNCH(0, 0, 0);
+      else if (m == 1) LLMT_RS3_LAUNCH(1, 0, 0);
+      else LLMT_RS3_LAUNCH(2, 0, 0);
+    }
+#undef LLMT_RS3_LAUNCH
   } else if (fillmode == 1) {
     if (skel == 1) LLMT_RS_LAUNCH(0, 4, 1);
+    else if (skel == 9 && m == 0) LLMT_RS_LAUNCH(0, 2, 9);  // slab epilogue only
     else if (skel == 2) LLMT_RS_LAUNCH(0, 2, 2);
     else if (skel == 3) LLMT_RS_LAUNCH(0, 2, 3);
     else if (slots == 2) {

@@ -151,6 +151,8 @@ long wgrad_gemm_det_ws_floats(int lda, int ldb, int M, int N, int K, int split, 
 // Ping-pong weight-gradient GEMM (gemm_wgrad_pp.hip): C[N,K] += dy^T x and, with `bias`,
 // bias[N] += colsum(dy).  `ws` holds wgrad_pp_ws_floats(...) floats (split slabs + bias parts).
 // mode: -1 auto, 0 slabs + fixed-order reduce, 2 fp32 atomics (ignored in deterministic mode).
+// Timing probe buffer of the SKEL 9 kernel (LLMT_WPP_SKEL=9; nullptr disables)
+hipError_t wgrad_pp_set_probe(void* buf);
 long wgrad_pp_ws_floats(int lda, int ldb, int M, int N, int K, int split, int mode, bool bias);
 hipError_t launch_wgrad_pp(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N, int K,
                            int split, int mode, float* ws, float* bias, hipStream_t stream);

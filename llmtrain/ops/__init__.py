@@ -328,9 +328,28 @@ def _gemm_rows(a, b, b_kn: bool, epilogue: int, bias=None, u=None, dbias=None, s
     return out, torch.cat([p[1] for p in parts])
 
 
+# GEMMs on the ping-pong kernel (csrc/gemm_pp.hip), by call site: LLMTRAIN_GEMM_PP = comma list of
+# fwd (linear_fwd), fwd_gelu, dx (linear_dx), dx_gelu (linear_dx_gelu_bwd); "all" = every one.  One
+# 256x256 tile per workgroup, no split-K: deterministic in both modes.
+_GPP_SITES = {"fwd", "fwd_gelu", "dx", "dx_gelu"}
+GEMM_PP = frozenset(_GPP_SITES if os.environ.get("LLMTRAIN_GEMM_PP", "") == "all"
+                    else [t for t in os.environ.get("LLMTRAIN_GEMM_PP", "").split(",") if t in _GPP_SITES])
+
+
+def _gpp_ok(site: str, x, w, bias=None, *, kn: bool = False) -> bool:
+    if not (site in GEMM_PP and _on_gpu(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
+        return False
+    k, n = x.shape[1], (w.shape[1] if kn else w.shape[0])
+    return (k % 64 == 0 and n % 8 == 0 and x.stride(1) == 1 and w.stride(1) == 1 and x.stride(0) % 8 == 0
+            and w.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+            and (bias is None or bias.data_ptr() % 8 == 0))
+
+
 def linear_fwd(x, w, bias=None):
-    """``x @ w^T + bias`` (nn.Linear forward, bf16 out).  GPU: the fused MFMA GEMM with the bias in
-    its epilogue where the shape allows, else hipBLASLt."""
+    """``x @ w^T + bias`` (nn.Linear forward, bf16 out).  GPU: the ping-pong GEMM when enabled, the
+    fused MFMA GEMM with the bias in its epilogue where the shape allows, else hipBLASLt."""
+    if _gpp_ok("fwd", x, w, bias):
+        return hip_ops().gemm_pp(x, w, bias, 0)[0]
     if _on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x, x.shape[1], w.shape[0], w, bias, op="fwd"):
         return _gemm_rows(x, w, False, 0, bias)[0]
     return torch.mm(x, w.t()) if bias is None else torch.addmm(bias, x, w.t())
@@ -339,6 +358,9 @@ def linear_fwd(x, w, bias=None):
 def linear_fwd_gelu(x, w, bias=None):
     """``u = x @ w^T + bias`` and ``g = gelu(u)`` (exact erf GELU of the bf16 ``u``, which the
     backward reads): on GPU the GELU rides in the GEMM epilogue, no separate pass over ``u``."""
+    if _gpp_ok("fwd_gelu", x, w, bias):
+        u, g = hip_ops().gemm_pp(x, w, bias, 1)
+        return u, g
     if _on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x, x.shape[1], w.shape[0], w, bias, op="fwd_gelu"):
         u, g = _gemm_rows(x, w, False, 1, bias)
         return u, g
@@ -348,6 +370,8 @@ def linear_fwd_gelu(x, w, bias=None):
 
 def linear_dx(dy, w):
     """``dy @ w`` (data gradient of nn.Linear with weight ``w [out, in]``)."""
+    if _gpp_ok("dx", dy, w, kn=True):
+        return hip_ops().gemm_pp(dy, w, None, 0, True)[0]
     if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy, dy.shape[1], w.shape[1], w, op="dx"):
         return _gemm_rows(dy, w, True, 0)[0]
     return torch.mm(dy, w)
@@ -387,6 +411,8 @@ def linear_dx_gelu_bwd(dy, w, u, dbias=None):
     """``du = (dy @ w) * gelu'(u)`` and ``dbias += colsum(du)``: the data gradient of the MLP
     projection fused with the GELU backward and the fc bias gradient (one GEMM epilogue on GPU
     instead of a GEMM plus a full read-modify pass over the [M, d_ff] activations)."""
+    if dbias is None and u.is_contiguous() and _gpp_ok("dx_gelu", dy, w, kn=True):
+        return hip_ops().gemm_pp(dy, w, None, 2, True, u)[0]
     if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy, dy.shape[1], w.shape[1], w, u, op="dx_gelu"):
         return _gemm_rows(dy, w, True, 2, None, u, dbias)[0]
     return gelu_bwd(torch.mm(dy, w), u, dbias)

@@ -342,6 +342,27 @@ def test_gemm_fused_bias_gelu(gpu_device, M, N, K, b_kn):
     _close(gl, torch.nn.functional.gelu(u.float()), 1e-2, 1e-2, "gelu(u)")
 
 
+# ---- ping-pong forward GEMM (csrc/gemm_pp.hip) ------------------------------------------------
+GPP_SHAPES = [(4096, 2304, 768), (513, 768, 3072), (1000, 200, 256), (300, 776, 128), (64, 50304, 768),
+              (131072, 768, 768)]  # bench M; ragged M / N; N past one tile row; the LM head's width
+
+
+@pytest.mark.parametrize("M,N,K", GPP_SHAPES)
+def test_gemm_pp_bias_gelu(gpu_device, M, N, K):
+    a, w, _, bias = _gemm_operands(M, N, K, False, gpu_device, 7 * M + N)
+    out, none = hip().gemm_pp(a, w, bias, 0)
+    assert none is None
+    ref = a.float() @ w.float().t() + bias.float()
+    _close(out, ref, 2e-2, 1e-2, "gemm_pp+bias")
+    out_nb, _ = hip().gemm_pp(a, w, None, 0)
+    _close(out_nb, a.float() @ w.float().t(), 2e-2, 1e-2, "gemm_pp")
+    u, gl = hip().gemm_pp(a, w, bias, 1)
+    assert torch.equal(u, out), "epilogue 1's pre-activation differs from epilogue 0"
+    _close(gl, torch.nn.functional.gelu(u.float()), 1e-2, 1e-2, "gelu(u)")
+    again, _ = hip().gemm_pp(a, w, bias, 0)
+    assert torch.equal(out, again), "gemm_pp is not deterministic"
+
+
 @pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
 @pytest.mark.parametrize("b_kn", [True, False])
 def test_gemm_fused_dgelu(gpu_device, M, N, K, b_kn):

@@ -74,6 +74,20 @@ def check() -> int:
             bad += not ok
             print(json.dumps({"case": name, "M": M, "N": N, "K": K, "kn": True, "epi": epi, "rel_err": err, "ok": ok}),
                   flush=True)
+    # out-projection dX + attention row constants (epilogue 3): dO = dy @ Wo, delta = per-head dO . O
+    T = 1024
+    for M in (4096, 2048):
+        dy = torch.randn(M, 768, device="cuda", dtype=torch.bfloat16)
+        w = (torch.randn(768, 768, device="cuda") * 768**-0.5).to(torch.bfloat16)
+        o = torch.randn(M, 768, device="cuda", dtype=torch.bfloat16)
+        d_o, delta = ops.gemm_pp(dy, w, None, 3, True, o, T)
+        ref = dy.float() @ w.float()
+        err = ((d_o.float() - ref).abs().max() / ref.abs().max()).item()
+        dref = (d_o.float() * o.float()).view(M // T, T, 12, 64).sum(-1).permute(0, 2, 1)
+        derr = ((delta - dref).abs().max() / dref.abs().max()).item()
+        ok = err < 1e-2 and derr < 1e-4
+        bad += not ok
+        print(json.dumps({"case": "dx_attn delta", "M": M, "rel_err": err, "delta_rel_err": derr, "ok": ok}), flush=True)
     return 1 if bad else 0
 
 
@@ -109,10 +123,13 @@ def time_dx(M: int, only: str = "") -> None:
         u = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
         gelu = name.endswith("gelu")
         flops = 2.0 * M * N * K
+        attn = name == "out_dx"
         variants = {
-            "pp": lambda: ops.gemm_pp(dy, w, None, 2 if gelu else 0, True, u if gelu else None),
+            "pp": lambda: ops.gemm_pp(dy, w, None, 2 if gelu else (3 if attn else 0), True,
+                                      u if (gelu or attn) else None, 1024 if attn else 0),
             "blas": lambda: torch.mm(dy, w),
-            "fused": lambda: ops.gemm_fused(dy[:16384], w, True, 2 if gelu else 0, None, u[:16384] if gelu else None),
+            "fused": lambda: ops.gemm_fused(dy[:16384], w, True, 2 if gelu else (3 if attn else 0), None,
+                                            u[:16384] if (gelu or attn) else None, None, 1024 if attn else 0),
         }
         for label, fn in variants.items():
             if only and label not in only.split(","):

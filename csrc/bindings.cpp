@@ -619,7 +619,7 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tens
 
 // ---- ping-pong GEMM: x @ w^T + bias (gelu of it for epi 1); kn: x @ w (epi 2: * gelu'(u)) -------
 std::tuple<Tensor, c10::optional<Tensor>> gemm_pp(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
-                                                  int64_t epi, bool kn, const c10::optional<Tensor>& u) {
+                                                  int64_t epi, bool kn, const c10::optional<Tensor>& u, int64_t seq_len) {
   check_gpu(x, "x");
   check_gpu(w, "w");
   check_dtype(x, at::kBFloat16, "x");
@@ -627,7 +627,8 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_pp(const Tensor& x, const Tensor&
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1, "gemm_pp: 2D row-major operands");
   const int64_t M = x.size(0), K = x.size(1), N = kn ? w.size(1) : w.size(0);
   TORCH_CHECK((kn ? w.size(0) : w.size(1)) == K, "gemm_pp: inner dimensions differ");
-  TORCH_CHECK(kn ? (epi == 0 || epi == 2) : (epi == 0 || epi == 1), "gemm_pp: epi 0 / 1 (forward) or 0 / 2 (kn)");
+  TORCH_CHECK(kn ? (epi == 0 || epi == 2 || epi == 3) : (epi == 0 || epi == 1),
+              "gemm_pp: epi 0 / 1 (forward) or 0 / 2 / 3 (kn)");
   TORCH_CHECK(llmt::gemm_pp_supported((int)M, (int)N, (int)K, (int)x.stride(0), (int)w.stride(0), (int)N, kn),
               "gemm_pp: needs K % 64 == 0, N % 8 == 0, 16-byte row strides");
   TORCH_CHECK((uintptr_t)x.data_ptr() % 16 == 0 && (uintptr_t)w.data_ptr() % 16 == 0, "gemm_pp: 16-byte aligned operands");
@@ -647,8 +648,14 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_pp(const Tensor& x, const Tensor&
     out2 = at::empty({M, N}, x.options());
     c2 = out2->data_ptr();
   }
-  if (epi == 2) {
-    TORCH_CHECK(u.has_value(), "gemm_pp: epi 2 needs u");
+  float* dptr = nullptr;
+  if (epi == 3) {
+    TORCH_CHECK(seq_len > 0 && M % seq_len == 0 && N % 64 == 0, "gemm_pp: epi 3 needs seq_len | M, 64 | N");
+    out2 = at::empty({M / seq_len, N / 64, seq_len}, x.options().dtype(at::kFloat));
+    dptr = out2->data_ptr<float>();
+  }
+  if (epi >= 2) {
+    TORCH_CHECK(u.has_value(), "gemm_pp: epi 2 / 3 needs u");
     check_gpu(*u, "u");
     check_dtype(*u, at::kBFloat16, "u");
     TORCH_CHECK(u->dim() == 2 && u->size(0) == M && u->size(1) == N && u->is_contiguous(), "gemm_pp: u must be [M, N]");
@@ -656,7 +663,8 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_pp(const Tensor& x, const Tensor&
   }
   if (M > 0)
     check_hip(llmt::launch_gemm_pp(x.data_ptr(), (int)x.stride(0), w.data_ptr(), (int)w.stride(0), bptr,
-                                   out.data_ptr(), c2, (int)N, (int)M, (int)N, (int)K, (int)epi, kn, cur_stream()),
+                                   out.data_ptr(), c2, (int)N, (int)M, (int)N, (int)K, (int)epi, kn, dptr,
+                                   (int)seq_len, cur_stream()),
               "gemm_pp");
   return {out, out2};
 }
@@ -766,7 +774,7 @@ TORCH_LIBRARY(llmtrain_hip, m) {
   m.def("wgrad_gemm(Tensor dy, Tensor x, Tensor(a!) c, int split=0, int tile=0, int pipe=-1) -> ()");
   m.def("wgrad_pp_probe(Tensor buf) -> ()");
   m.def("wgrad_gemm_pp(Tensor dy, Tensor x, Tensor(a!) c, Tensor(b!)? bias=None, int split=0, int mode=-1) -> ()");
-  m.def("gemm_pp(Tensor x, Tensor w, Tensor? bias=None, int epi=0, bool kn=False, Tensor? u=None) -> (Tensor, Tensor?)");
+  m.def("gemm_pp(Tensor x, Tensor w, Tensor? bias=None, int epi=0, bool kn=False, Tensor? u=None, int seq_len=0) -> (Tensor, Tensor?)");
   m.def("gemm_fused(Tensor a, Tensor b, bool b_kn, int epilogue, Tensor? bias=None, Tensor? u=None,"
         " Tensor(a!)? dbias=None, int seq_len=0) -> (Tensor, Tensor?)");
   m.def("sumsq(Tensor x) -> Tensor");

@@ -28,7 +28,9 @@
 //
 // Epilogues (EPI): 0 = bf16(acc + bias); 1 = u = bf16(acc + bias) and bf16(gelu(u)) (fc forward,
 // the pre-activation is kept for the backward); 2 = bf16(acc * gelu'(u)) with u read from C2's
-// place (proj dX fused with the GELU backward).
+// place (proj dX fused with the GELU backward); 3 = bf16(acc) and delta[b, h, t] = sum_d dO * O
+// over each 64-wide head with O read from C2's place (out-proj dX fused with the attention
+// backward's row constants).
 #include <algorithm>
 #include <cstdlib>
 
@@ -111,7 +113,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_pp_kernel(const bf16_raw* __
                                                              const bf16_raw* __restrict__ W, int ldw,
                                                              const bf16_raw* __restrict__ bias,
                                                              bf16_raw* __restrict__ C, bf16_raw* __restrict__ C2,
-                                                             int ldc, int M, int N, int K, int tiles_n, int nwg) {
+                                                             int ldc, int M, int N, int K, int tiles_n, int nwg,
+                                                             float* __restrict__ delta, int T) {
   __shared__ __attribute__((aligned(16))) bf16_raw smem[NS * SLOT / 2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -281,6 +284,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_pp_kernel(const bf16_raw* __
 #pragma unroll
   for (int j = 0; j < FB; ++j) {
     const int mo = (mrow + 16 * j - m0) * ldc * 2;
+    float dot[2] = {0.f, 0.f};  // EPI 3: this lane's part of the row dot of each of the wave's 2 heads
 #pragma unroll
     for (int i = 0; i < FA; ++i) {
       const int n = nb + 16 * i;
@@ -299,10 +303,31 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_pp_kernel(const bf16_raw* __
       const bf16_raw u0 = f2bf(v[0]), u1 = f2bf(v[1]), u2 = f2bf(v[2]), u3 = f2bf(v[3]);
       const u32x2 pu = {(unsigned)u0 | ((unsigned)u1 << 16), (unsigned)u2 | ((unsigned)u3 << 16)};
       __builtin_amdgcn_raw_buffer_store_b64(pu, rc, mo + n * 2, 0, 0);
+      if (EPI == 3) {  // delta: the bf16 dO the attention backward reads, times O (from C2's place)
+        const u32x2 oo = __builtin_amdgcn_raw_buffer_load_b64(rc2, mo + n * 2, 0, 0);
+        dot[i >> 2] = fmaf(bf2f(u0), __uint_as_float(oo[0] << 16), dot[i >> 2]);
+        dot[i >> 2] = fmaf(bf2f(u1), __uint_as_float(oo[0] & 0xffff0000u), dot[i >> 2]);
+        dot[i >> 2] = fmaf(bf2f(u2), __uint_as_float(oo[1] << 16), dot[i >> 2]);
+        dot[i >> 2] = fmaf(bf2f(u3), __uint_as_float(oo[1] & 0xffff0000u), dot[i >> 2]);
+      }
       if (EPI == 1) {
         const float g0 = gelu_erf(bf2f(u0)), g1 = gelu_erf(bf2f(u1)), g2 = gelu_erf(bf2f(u2)), g3 = gelu_erf(bf2f(u3));
         const u32x2 pg = {(unsigned)f2bf(g0) | ((unsigned)f2bf(g1) << 16), (unsigned)f2bf(g2) | ((unsigned)f2bf(g3) << 16)};
         __builtin_amdgcn_raw_buffer_store_b64(pg, rc2, mo + n * 2, 0, 0);
+      }
+    }
+    if (EPI == 3) {  // the 4 lanes g = 0..3 of a row hold its 64 head columns (N % 64 == 0)
+      const int m = mrow + 16 * j;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        float d = dot[hh];
+        d += __shfl_xor(d, 16, 64);
+        d += __shfl_xor(d, 32, 64);
+        const int head = (n0 + 128 * wn + 64 * hh) >> 6;
+        if (g == 0 && m < M && 64 * head < N) {
+          const int bb = m / T, t = m - bb * T;
+          delta[((long)bb * (N >> 6) + head) * T + t] = d;
+        }
       }
     }
   }
@@ -317,9 +342,10 @@ bool gemm_pp_supported(int M, int N, int K, int ldx, int ldw, int ldc, bool kn) 
 }
 
 hipError_t launch_gemm_pp(const void* x, int ldx, const void* w, int ldw, const void* bias, void* c, void* c2, int ldc,
-                          int M, int N, int K, int epi, bool kn, hipStream_t stream) {
-  if (!gemm_pp_supported(M, N, K, ldx, ldw, ldc, kn) || (epi >= 1 && c2 == nullptr) || epi < 0 || epi > 2)
+                          int M, int N, int K, int epi, bool kn, float* delta, int T, hipStream_t stream) {
+  if (!gemm_pp_supported(M, N, K, ldx, ldw, ldc, kn) || (epi >= 1 && c2 == nullptr) || epi < 0 || epi > 3)
     return hipErrorInvalidValue;
+  if (epi == 3 && (delta == nullptr || T <= 0 || M % T != 0 || N % 64 != 0)) return hipErrorInvalidValue;
   const int tiles_m = (M + gpp::TW - 1) / gpp::TW, tiles_n = (N + gpp::TW - 1) / gpp::TW;
   const int nwg = tiles_m * tiles_n;
   static const int fill = [] {
@@ -329,7 +355,7 @@ hipError_t launch_gemm_pp(const void* x, int ldx, const void* w, int ldw, const 
 #define LLMT_GPP_LAUNCH(E, F, KN)                                                                                 \
   hipLaunchKernelGGL((gpp::gemm_pp_kernel<E, F, KN>), dim3(nwg), dim3(gpp::kThreads), 0, stream,                   \
                      (const bf16_raw*)x, ldx, (const bf16_raw*)w, ldw, (const bf16_raw*)bias, (bf16_raw*)c,          \
-                     (bf16_raw*)c2, ldc, M, N, K, tiles_n, nwg)
+                     (bf16_raw*)c2, ldc, M, N, K, tiles_n, nwg, delta, T)
 #define LLMT_GPP_FILLS(E, KN)            \
   if (fill == 1) LLMT_GPP_LAUNCH(E, 1, KN); \
   else LLMT_GPP_LAUNCH(E, 3, KN);
@@ -340,6 +366,7 @@ hipError_t launch_gemm_pp(const void* x, int ldx, const void* w, int ldw, const 
   } else {
     if (epi == 0) { LLMT_GPP_FILLS(0, true) }
     else if (epi == 2) { LLMT_GPP_FILLS(2, true) }
+    else if (epi == 3) { LLMT_GPP_FILLS(3, true) }
     else return hipErrorInvalidValue;
   }
 #undef LLMT_GPP_FILLS

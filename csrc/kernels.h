@@ -191,10 +191,11 @@ hipError_t launch_gemm_fused(const GemmFusedArgs& args, hipStream_t stream);
 
 // Ping-pong GEMM (gemm_pp.hip): c[M,N] = bf16(x[M,K] w[N,K]^T + bias) (kn = false; epi 1 also
 // c2 = bf16(gelu(c))) or c = bf16(x[M,K] w[K,N]) (kn = true, data gradient; epi 2: c = bf16(acc *
-// gelu'(c2)), c2 = the pre-activation u).  Needs K % 64 == 0, N % 8 == 0 (gemm_pp_supported).
+// gelu'(c2)), c2 = the pre-activation u; epi 3: delta[b, h, t] = sum over head h's 64 columns of
+// c * c2 (c2 = the attention output O), T = sequence length).  Needs K % 64 == 0, N % 8 == 0.
 bool gemm_pp_supported(int M, int N, int K, int ldx, int ldw, int ldc, bool kn);
 hipError_t launch_gemm_pp(const void* x, int ldx, const void* w, int ldw, const void* bias, void* c, void* c2, int ldc,
-                          int M, int N, int K, int epi, bool kn, hipStream_t stream);
+                          int M, int N, int K, int epi, bool kn, float* delta, int T, hipStream_t stream);
 inline long gemm_fused_ws_floats(int M, int N) {
   const int nparts = (M + 127) / 128;
   return (long)nparts * N + colsum_scratch_floats(nparts, N);

@@ -329,9 +329,10 @@ def _gemm_rows(a, b, b_kn: bool, epilogue: int, bias=None, u=None, dbias=None, s
 
 
 # GEMMs on the ping-pong kernel (csrc/gemm_pp.hip), by call site: LLMTRAIN_GEMM_PP = comma list of
-# fwd (linear_fwd), fwd_gelu, dx (linear_dx), dx_gelu (linear_dx_gelu_bwd); "all" = every one.  One
+# fwd (linear_fwd), fwd_gelu, dx (linear_dx), dx_gelu (linear_dx_gelu_bwd), dx_attn
+# (linear_dx_attn); "all" = every one.  One
 # 256x256 tile per workgroup, no split-K: deterministic in both modes.
-_GPP_SITES = {"fwd", "fwd_gelu", "dx", "dx_gelu"}
+_GPP_SITES = {"fwd", "fwd_gelu", "dx", "dx_gelu", "dx_attn"}
 GEMM_PP = frozenset(_GPP_SITES if os.environ.get("LLMTRAIN_GEMM_PP", "") == "all"
                     else [t for t in os.environ.get("LLMTRAIN_GEMM_PP", "").split(",") if t in _GPP_SITES])
 
@@ -426,6 +427,9 @@ def linear_dx_attn(dy, w, att, seqlen: int, v_bias_grad=None, head_dim: int = 64
     replacing the separate pass that re-read dO and O.  Returns ``(dO, delta)``; ``delta`` is None
     when the GEMM is not taken (the attention backward then computes it itself, and the caller
     must leave ``v_bias_grad`` to it)."""
+    if (v_bias_grad is None and head_dim == 64 and dy.shape[0] % seqlen == 0 and w.shape[1] % 64 == 0
+            and att.is_contiguous() and _gpp_ok("dx_attn", dy, w, kn=True)):
+        return tuple(hip_ops().gemm_pp(dy, w, None, 3, True, att, seqlen))
     if (
         _on_gpu(dy)
         and dy.dtype == torch.bfloat16

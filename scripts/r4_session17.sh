@@ -33,5 +33,5 @@ for r in 1 2; do
 done
 # step A/B: forward GEMMs on the ping-pong kernel (only if its numerics passed)
 if ! grep -q '"ok": false' $O/gpp_check.txt && grep -q '"ok": true' $O/gpp_check.txt; then
-  bash scripts/abn.sh "LLMTRAIN_GEMM_PP=none" "LLMTRAIN_GEMM_PP=fwd,fwd_gelu" "LLMTRAIN_GEMM_PP=dx_gelu" "LLMTRAIN_GEMM_PP=all" -- --steps 10 --warmup 3 > $O/ab_gemm_pp_mb128.txt 2>&1
+  bash scripts/abn.sh "LLMTRAIN_GEMM_PP=none" "LLMTRAIN_GEMM_PP=fwd,fwd_gelu" "LLMTRAIN_GEMM_PP=dx_gelu,dx_attn" "LLMTRAIN_GEMM_PP=all" -- --steps 10 --warmup 3 > $O/ab_gemm_pp_mb128.txt 2>&1
 fi

@@ -363,6 +363,31 @@ def test_gemm_pp_bias_gelu(gpu_device, M, N, K):
     assert torch.equal(out, again), "gemm_pp is not deterministic"
 
 
+GPP_DX_SHAPES = [(4096, 768, 3072), (1000, 3072, 768), (2048, 768, 768), (300, 776, 128)]
+
+
+@pytest.mark.parametrize("M,N,K", GPP_DX_SHAPES)
+def test_gemm_pp_dx_epilogues(gpu_device, M, N, K):
+    """Data-gradient layout (dX = dY W, W [K, N]): plain, GELU backward (du = acc * gelu'(u)) and,
+    for whole 1024-token sequences, the attention row constants delta = per-head dO . O."""
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    dy = (torch.randn(M, K, generator=g) / math.sqrt(K)).to(gpu_device, torch.bfloat16)
+    w = torch.randn(K, N, generator=g).to(gpu_device, torch.bfloat16)
+    u = torch.randn(M, N, generator=g).to(gpu_device, torch.bfloat16)
+    ref = dy.float() @ w.float()
+    out, _ = hip().gemm_pp(dy, w, None, 0, True)
+    _close(out, ref, 2e-2, 1e-2, "gemm_pp kn")
+    du, _ = hip().gemm_pp(dy, w, None, 2, True, u)
+    x = u.float().requires_grad_(True)
+    torch.nn.functional.gelu(x).backward(torch.ones_like(x))
+    _close(du, out.float() * x.grad, 3e-2, 2e-2, "gemm_pp kn gelu'")
+    if M % 1024 == 0 and N % 64 == 0:
+        d_o, delta = hip().gemm_pp(dy, w, None, 3, True, u, 1024)
+        assert torch.equal(d_o, out)
+        dref = (d_o.float() * u.float()).view(M // 1024, 1024, N // 64, 64).sum(-1).permute(0, 2, 1)
+        _close(delta, dref, 1e-3, 1e-4, "gemm_pp delta")
+
+
 @pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
 @pytest.mark.parametrize("b_kn", [True, False])
 def test_gemm_fused_dgelu(gpu_device, M, N, K, b_kn):

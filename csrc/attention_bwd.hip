@@ -223,7 +223,7 @@ __device__ __forceinline__ float swap_pair(float x) {
 // 16 rows a ds_read_b128 lane group touches land on 16 distinct chunks (all 64 banks)
 __device__ __forceinline__ int kt_off(int d, int key) { return d * kKvBlk + ((((key >> 3) ^ (d & 15))) << 3) + (key & 7); }
 
-template <bool DROPOUT, bool KMASK, bool SMALLHD, bool SPLIT, bool STAGGER = false>
+template <bool DROPOUT, bool KMASK, bool SMALLHD, bool SPLIT>
 __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __restrict__ qkv,
                                                           const bf16_raw* __restrict__ dout,
                                                           const float* __restrict__ lse,
@@ -458,137 +458,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
   __syncthreads();
   BWD_PROBE(1);
 
-  if constexpr (STAGGER) {
-  // dQ of one tile as a function (the STAGGER loop forms it at two places)
-  auto dq_tile = [&](const int q0, const bf16_raw* dsimg, float* accp, f32x4 prev0, f32x4 prev1) {
-      const int i = lane & 15, g = lane >> 4;
-      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-      typedef short short8v __attribute__((ext_vector_type(8)));
-      // software pipeline: the operands of step ks + 3 are read while step ks's MFMAs run (12 LDS
-      // reads in flight, inside lgkmcnt's 15).  The compiler's own schedule read one pair ahead
-      // and waited on LDS latency before every MFMA (~2.2k cycles for 256 cycles of MFMA);
-      // hoisting all 8 steps' reads spilled (address registers: the K^T swizzle makes every step's
-      // offset distinct).
-      constexpr int kSteps = kKvBlk / 32, kAhead = 3;
-      bf16x8 av[kSteps], b0[kSteps], b1[kSteps];
-      auto read_step = [&](int ks) {
-        const int krow = 32 * ks + 8 * g + (i >> 2);
-        const int qcol = 16 * qt_dq + 4 * (i & 3);
-        const short4v a_lo = tr_read(dsimg, krow, qcol);
-        const short4v a_hi = tr_read(dsimg, krow + 4, qcol);
-        const short8v a8 = {a_lo[0], a_lo[1], a_lo[2], a_lo[3], a_hi[0], a_hi[1], a_hi[2], a_hi[3]};
-        av[ks] = __builtin_bit_cast(bf16x8, a8);
-        const int kc = 32 * ks + 8 * g;  // first of this lane's 8 keys
-        b0[ks] = *reinterpret_cast<const bf16x8*>(&kt_lds[kt_off(32 * dp_dq + i, kc)]);
-        b1[ks] = *reinterpret_cast<const bf16x8*>(&kt_lds[kt_off(32 * dp_dq + 16 + i, kc)]);
-      };
-#pragma unroll
-      for (int ks = 0; ks < kAhead; ++ks) read_step(ks);
-#pragma unroll
-      for (int ks = 0; ks < kSteps; ++ks) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (ks + kAhead < kSteps) read_step(ks + kAhead);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[ks], b0[ks], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[ks], b1[ks], acc1, 0, 0, 0);
-      }
-      // dQ accumulates in fp32 across the key blocks: rows below this key block (every earlier block
-      // contributed) add the partial read at the top of the tile; rows of the block's own 256-row
-      // band get no later contribution, so they leave as bf16 straight into dqkv (scaled), all other
-      // rows go back to the private buffer.  Rows past T and dims past hd are zero (zero Q rows /
-      // masked P; zero K^T dims).
-      acc0 += prev0;
-      acc1 += prev1;
-      // lanes i and i^1 swap half their rows so each lane stores whole dwords (two adjacent
-      // columns): even lanes rows 0,1, odd rows 2,3
-      const int p = i & 1;
-      if (split) {  // this key block's bf16 partial plane [kb][b, h, t, 64]
-        bf16_raw* plane = reinterpret_cast<bf16_raw*>(dq_acc) + ((long)kb * gridDim.x + bh) * T * kHD;
-        const int dcol = 32 * dp_dq + (i & ~1);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int r = p ? 2 + j : j;
-          const int qq = q0 + 16 * qt_dq + 4 * g + r;
-          const float s0 = swap_pair(p ? acc0[j] : acc0[2 + j]);
-          const float s1 = swap_pair(p ? acc1[j] : acc1[2 + j]);
-          const float o0 = p ? acc0[2 + j] : acc0[j], o1 = p ? acc1[2 + j] : acc1[j];
-          const uint32_t w0 = (uint32_t)f2bf((p ? s0 : o0) * scale) | ((uint32_t)f2bf((p ? o0 : s0) * scale) << 16);
-          const uint32_t w1 = (uint32_t)f2bf((p ? s1 : o1) * scale) | ((uint32_t)f2bf((p ? o1 : s1) * scale) << 16);
-          if (qq < T) {
-            bf16_raw* dst = plane + (long)qq * kHD + dcol;
-            *reinterpret_cast<uint32_t*>(dst) = w0;
-            *reinterpret_cast<uint32_t*>(dst + 16) = w1;
-          }
-        }
-      } else if (q0 >= kblk0 + kKvBlk) {
-        *reinterpret_cast<f32x4*>(accp) = acc0;
-        *reinterpret_cast<f32x4*>(accp + 4) = acc1;
-      } else {
-        const int dcol = 32 * dp_dq + (i & ~1);  // even column of this lane's pair
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int r = p ? 2 + j : j;  // the row this lane stores
-          const int qq = q0 + 16 * qt_dq + 4 * g + r;
-          const float s0 = swap_pair(p ? acc0[j] : acc0[2 + j]);
-          const float s1 = swap_pair(p ? acc1[j] : acc1[2 + j]);
-          const float o0 = p ? acc0[2 + j] : acc0[j], o1 = p ? acc1[2 + j] : acc1[j];
-          const uint32_t w0 = (uint32_t)f2bf((p ? s0 : o0) * scale) | ((uint32_t)f2bf((p ? o0 : s0) * scale) << 16);
-          const uint32_t w1 = (uint32_t)f2bf((p ? s1 : o1) * scale) | ((uint32_t)f2bf((p ? o1 : s1) * scale) << 16);
-          if (qq < T) {
-            bf16_raw* dst = dqkv + ((long)b * T + qq) * row_stride + (long)h * hd + dcol;
-            if (!SMALLHD || dcol < hd) *reinterpret_cast<uint32_t*>(dst) = w0;
-            if (!SMALLHD || dcol + 16 < hd) *reinterpret_cast<uint32_t*>(dst + 16) = w1;
-          }
-        }
-        qsum0 += (acc0[0] + acc0[1] + acc0[2] + acc0[3]) * scale;
-        qsum1 += (acc1[0] + acc1[1] + acc1[2] + acc1[3]) * scale;
-      }
-  };
-  // STAGGER: waves 4-7 form each tile's dQ after the NEXT tile's phase A instead of before it, so on
-  // every SIMD one wave's MFMA-only dQ runs beside its partner's VALU-heavy phase A (MI355X_MICROARCH
-  // "Two waves per SIMD", item 9).  dS images stay double-buffered: a lagging wave reads tile it-1's
-  // image during interval it, while phase A of tile it writes the other one.  It issues its DMA after
-  // that dQ, so the counted wait before the barrier still leaves exactly that DMA in flight.
-  const bool lag = wave >= 4;
-  int it = 0, cur3 = 0;
-  for (int q0 = kblk0; q0 < T; q0 += kQTile, ++it) {
-    const int cur = it & 1;
-    const bool more = it + 1 < ntiles, more2 = it + 2 < ntiles;
-    if (more) load_rowc(q0 + kQTile);
-    float* accp = dq_acc + ((((long)bh * ntq + q0 / kQTile) * kBwdWaves + wave) * 64 + lane) * 8;
-    float* paccp = lag ? accp - kBwdWaves * 64 * 8 : accp;  // the tile whose dQ this interval forms
-    f32x4 prev0 = {0.f, 0.f, 0.f, 0.f}, prev1 = prev0;
-    if (!split && kb > 0 && (!lag || it > 0)) {
-      prev0 = *reinterpret_cast<const f32x4*>(paccp);
-      prev1 = *reinterpret_cast<const f32x4*>(paccp + 4);
-    }
-    const int nxt3 = cur3 == 2 ? 0 : cur3 + 1, nxt3b = nxt3 == 2 ? 0 : nxt3 + 1;
-    if (!lag && more2) dma_tile(q0 + 2 * kQTile, nxt3b);
-    phase_a(q0 >= kblk0 + kKvBlk && q0 + kQTile <= T, q0, qd_lds[cur3][0], qd_lds[cur3][1], rowc_lds[cur], ds_lds[cur]);
-    if (more) store_rowc(cur ^ 1);
-    auto tile_barrier = [&] {
-      if (more2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    };
-    if (!lag) tile_barrier();
-    cur3 = nxt3;
-    if (!lag || it > 0) dq_tile(lag ? q0 - kQTile : q0, ds_lds[lag ? cur ^ 1 : cur], paccp, prev0, prev1);
-    if (lag) {
-      if (more2) dma_tile(q0 + 2 * kQTile, nxt3b);
-      tile_barrier();
-    }
-  }
-  if (lag && it > 0) {  // a lagging wave's last dQ (the loop's last barrier completed its dS image)
-    const int q0l = kblk0 + (it - 1) * kQTile;
-    float* accp = dq_acc + ((((long)bh * ntq + q0l / kQTile) * kBwdWaves + wave) * 64 + lane) * 8;
-    f32x4 prev0 = {0.f, 0.f, 0.f, 0.f}, prev1 = prev0;
-    if (!split && kb > 0) {
-      prev0 = *reinterpret_cast<const f32x4*>(accp);
-      prev1 = *reinterpret_cast<const f32x4*>(accp + 4);
-    }
-    dq_tile(q0l, ds_lds[(it - 1) & 1], accp, prev0, prev1);
-  }
-  } else {
   int it = 0, cur3 = 0;
   for (int q0 = kblk0; q0 < T; q0 += kQTile, ++it) {
     const int cur = it & 1;
@@ -706,7 +575,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
       }
     }
     BWD_PROBE(4 + 3 * it);
-  }
   }
 
   // ---- dK = scale * dK^T, dV = dV^T  -> dqkv[b, key, 1|2, h, :] ------------------------------
@@ -1140,15 +1008,6 @@ static void launch_bwd_variant(dim3 grid, hipStream_t stream, const bf16_raw* qk
                                float* dq_acc, float* vparts, float* qparts, const AttnDims& d, int nkb,
                                DropoutArgs dr) {
   set_bwd_prio_once();
-  static const bool stagger = [] {  // LLMT_ATTN_BWD_STAGGER=1: the dQ stagger (A/B knob)
-    const char* e = std::getenv("LLMT_ATTN_BWD_STAGGER");
-    return e != nullptr && std::atoi(e) != 0;
-  }();
-  if (stagger && !DROPOUT && !KMASK && !SMALLHD && grid.y == 1) {
-    hipLaunchKernelGGL((attn::attn_bwd_kernel<false, false, false, false, true>), grid, dim3(512), 0, stream, qkv,
-                       dout, lse, delta, dqkv, dq_acc, vparts, qparts, d.T, d.H, nkb, dr, d.hd, d.scale, d.key_valid);
-    return;
-  }
   if (grid.y > 1)
     hipLaunchKernelGGL((attn::attn_bwd_kernel<DROPOUT, KMASK, SMALLHD, true>), grid, dim3(512), 0, stream, qkv, dout,
                        lse, delta, dqkv, dq_acc, vparts, qparts, d.T, d.H, nkb, dr, d.hd, d.scale, d.key_valid);

@@ -255,7 +255,7 @@ def attn_bwd(
 # each GEMM alone is ahead of hipBLASLt at 64K: its persistent, statically scheduled 160 KiB-LDS
 # workgroups start late on CUs still draining the previous kernel.  Above this many A bytes the
 # engine stays on hipBLASLt.
-FGEMM_MAX_A_BYTES = 64 * 2**20
+FGEMM_MAX_A_BYTES = int(float(os.environ.get("LLMTRAIN_FGEMM_MAX_A_MB", "64")) * 2**20)  # A/B knob
 # Ops that take the fused GEMM at any A size.  dx_gelu: the MLP-projection dX with GELU backward +
 # fc-bias grad in the epilogue replaces a hipBLASLt GEMM plus a full [M, 4d] read-modify pass, and
 # wins in the whole 124M step (same-box, micro-batch 128: +0.9 %, 994.9k/995.5k vs 985.8k/986.8k

@@ -256,6 +256,8 @@ def attn_bwd(
 # workgroups start late on CUs still draining the previous kernel.  Above this many A bytes the
 # engine stays on hipBLASLt.
 FGEMM_MAX_A_BYTES = int(float(os.environ.get("LLMTRAIN_FGEMM_MAX_A_MB", "64")) * 2**20)  # A/B knob
+# Ops that stay on the library GEMM at every size (outside deterministic mode's "ours" schedule)
+FGEMM_NEVER = frozenset(t for t in os.environ.get("LLMTRAIN_FGEMM_NEVER", "").split(",") if t)
 # Ops that take the fused GEMM at any A size.  dx_gelu: the MLP-projection dX with GELU backward +
 # fc-bias grad in the epilogue replaces a hipBLASLt GEMM plus a full [M, 4d] read-modify pass, and
 # wins in the whole 124M step (same-box, micro-batch 128: +0.9 %, 994.9k/995.5k vs 985.8k/986.8k
@@ -294,6 +296,8 @@ def _fgemm_ok(a: torch.Tensor, k: int, n: int, *others: torch.Tensor | None, op:
         _det_fallback(f"GEMM {op or 'linear'} K={k} N={n} (needs K % 64 == 0, K >= 256, N % 8 == 0)")
         return False
     if a.numel() * a.element_size() > FGEMM_MAX_A_BYTES and op not in FGEMM_ANY_SIZE and not _POLICY["gemm_all_ours"]:
+        return False
+    if op in FGEMM_NEVER and not _POLICY["gemm_all_ours"]:
         return False
     if not all(t is None or t.data_ptr() % 16 == 0 for t in (a, *others)):
         _det_fallback(f"GEMM {op or 'linear'} with an operand not 16-byte aligned")
@@ -346,12 +350,40 @@ def _gpp_ok(site: str, x, w, bias=None, *, kn: bool = False) -> bool:
             and (bias is None or bias.data_ptr() % 8 == 0))
 
 
+_TUNED_BIAS_GEMMS: set[tuple[int, int, int]] | None = None
+
+
+def _library_tuned_bias_gemm(m: int, n: int, k: int) -> bool:
+    """Whether the shipped TunableOp table (llmtrain/runtime/tuned/) holds a measured library
+    solution for the bias GEMM ``[m, k] @ [n, k]^T + bias``: such shapes were timed against our
+    kernel when the table was made (micro-batch 32: qkv 0.109 vs 0.116 ms, out 0.041 vs 0.053 ms,
+    profiles/r4/mb32/) and stay on the library."""
+    global _TUNED_BIAS_GEMMS
+    if _TUNED_BIAS_GEMMS is None:
+        from ..runtime.tuning import TUNED_TABLE, tuned_gemms_active
+
+        if not tuned_gemms_active():  # not (yet) loaded in this process: nothing is routed by it
+            return False
+        shapes: set[tuple[int, int, int]] = set()
+        if TUNED_TABLE.is_file():
+            for line in TUNED_TABLE.read_text().splitlines():
+                parts = line.split(",")
+                if len(parts) >= 2 and parts[0] == "GemmAndBiasTunableOp_BFloat16_TN" and parts[1].startswith("tn_"):
+                    dims = parts[1].split("_")
+                    shapes.add((int(dims[2]), int(dims[1]), int(dims[3])))  # tn_{N}_{M}_{K}: (M, N, K)
+        _TUNED_BIAS_GEMMS = shapes
+    return (m, n, k) in _TUNED_BIAS_GEMMS
+
+
 def linear_fwd(x, w, bias=None):
     """``x @ w^T + bias`` (nn.Linear forward, bf16 out).  GPU: the ping-pong GEMM when enabled, the
-    fused MFMA GEMM with the bias in its epilogue where the shape allows, else hipBLASLt."""
+    fused MFMA GEMM with the bias in its epilogue where the shape allows and the library has no
+    measured solution for it, else hipBLASLt."""
     if _gpp_ok("fwd", x, w, bias):
         return hip_ops().gemm_pp(x, w, bias, 0)[0]
-    if _on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x, x.shape[1], w.shape[0], w, bias, op="fwd"):
+    if (_on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x, x.shape[1], w.shape[0], w, bias, op="fwd")
+            and (_POLICY["gemm_all_ours"] or bias is None
+                 or not _library_tuned_bias_gemm(x.shape[0], w.shape[0], x.shape[1]))):
         return _gemm_rows(x, w, False, 0, bias)[0]
     return torch.mm(x, w.t()) if bias is None else torch.addmm(bias, x, w.t())
 

@@ -20,7 +20,7 @@ from pathlib import Path
 
 import torch
 
-__all__ = ["TUNED_TABLE", "enable_tuned_gemms"]
+__all__ = ["TUNED_TABLE", "enable_tuned_gemms", "tuned_gemms_active"]
 
 logger = logging.getLogger(__name__)
 
@@ -58,3 +58,8 @@ def enable_tuned_gemms(device: torch.device) -> bool:
                 logger.info("tuned GEMM table loaded: %s", TUNED_TABLE)
     _state["active"] = active
     return active
+
+
+def tuned_gemms_active() -> bool:
+    """Whether :func:`enable_tuned_gemms` loaded the shipped table in this process."""
+    return _state.get("active", False)

@@ -20,3 +20,19 @@ def test_table_is_well_formed_for_gfx950() -> None:
 
 def test_cpu_device_is_a_no_op() -> None:
     assert enable_tuned_gemms(torch.device("cpu")) is False
+
+
+def test_tuned_bias_gemm_shapes_route_to_the_library(monkeypatch) -> None:
+    """Bias-GEMM shapes with a measured library solution in the table (micro-batch 32 qkv / out
+    forward) are routed away from the fused GEMM; other shapes and an unloaded table are not."""
+    import llmtrain.ops as ops
+    from llmtrain.runtime import tuning
+
+    monkeypatch.setattr(ops, "_TUNED_BIAS_GEMMS", None)
+    assert ops._library_tuned_bias_gemm(32768, 2304, 768) is False  # table not loaded here
+    monkeypatch.setitem(tuning._state, "active", True)
+    assert ops._library_tuned_bias_gemm(32768, 2304, 768)  # qkv forward, micro-batch 32
+    assert ops._library_tuned_bias_gemm(32768, 768, 768)  # out-projection forward
+    assert ops._library_tuned_bias_gemm(131072, 3072, 768)  # fc forward, micro-batch 128
+    assert not ops._library_tuned_bias_gemm(32768, 3072, 768)  # fc forward at 32: fused GELU epilogue
+    assert not ops._library_tuned_bias_gemm(4096, 2304, 768)

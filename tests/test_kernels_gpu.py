@@ -73,7 +73,7 @@ def test_layernorm_bwd(gpu_device, M, d, with_proj, lowp):
         assert torch.equal(dp, torch.full((d,), 0.25, device=gpu_device))
 
 
-@pytest.mark.parametrize("M,V,Vp", [(256, 50257, 50304), (64, 16, 64), (33, 1000, 1024)])
+@pytest.mark.parametrize("M,V,Vp", [(256, 50257, 50304), (1000, 50257, 50304), (64, 16, 64), (33, 1000, 1024)])
 def test_cross_entropy_fwd_bwd(gpu_device, M, V, Vp):
     g = torch.Generator(device="cpu").manual_seed(V)
     logits = (3 * torch.randn(M, Vp, generator=g)).to(gpu_device, torch.bfloat16)

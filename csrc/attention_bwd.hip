@@ -362,9 +362,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
     for (int qs = 0; qs < 2; ++qs) {
       const int qb0 = q0 + 32 * qs;
       const bool active = full || (kw0 <= qb0 + 31 && kw0 < T && qb0 < T);  // wave-uniform
-      f32x16 ds;
+      bf16x8 sbs[2];  // dS packed to bf16: the dK^T operand and, as is, the dS^T image
       if (active) {
-        f32x16 p, dp;
+        f32x16 p, dp, ds;
         p = 0.f;
         dp = 0.f;
 #pragma unroll
@@ -419,7 +419,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
           const bf16x8 pb = pack_acc8(p, st);
-          const bf16x8 sb = pack_acc8(ds, st);
+          sbs[st] = pack_acc8(ds, st);
+          const bf16x8 sb = sbs[st];
 #pragma unroll
           for (int dt = 0; dt < 2; ++dt) {
             const bf16x8 doa = lds_tr_read_operand(do_lds, 32 * qs + 16 * st + 4 * half, dt * 32, lane);
@@ -429,15 +430,17 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(const bf16_raw* __rest
           }
         }
       } else {
-        ds = 0.f;
+        const bf16x8 z = {};
+        sbs[0] = z;
+        sbs[1] = z;
       }
       // dS^T image [key][q]: this lane's key, q rows 32 qs + 8g + 4h .. +3 (one 8-byte write each)
       const int kl = 32 * wave + col;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        ushort4_t v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = f2bf(ds[4 * g + i]);
+        const ushort8_t u = __builtin_bit_cast(ushort8_t, sbs[g >> 1]);  // rows 8(g>>1) .. +7
+        const int o = 4 * (g & 1);
+        const ushort4_t v = {u[o], u[o + 1], u[o + 2], u[o + 3]};
         *reinterpret_cast<ushort4_t*>(&dsimg[tile_elem_off(kl, 32 * qs + 8 * g + 4 * half)]) = v;
       }
       // keep the two sub-tiles' live ranges apart: overlapping them exceeds the 256-VGPR budget

@@ -32,7 +32,7 @@ def load() -> bool:
         if _state["error"] is not None:
             return False
         default = DEBUG_EXT_PATH if os.environ.get("LLMTRAIN_DEBUG_KERNELS", "0") == "1" else EXT_PATH
-        path = Path(os.environ.get("LLMTRAIN_HIP_EXT", default))
+        path = Path(os.environ.get("LLMTRAIN_HIP_EXT") or default)  # empty: the default
         if not path.exists():
             _state["error"] = f"{path} not found (build it with `python -m llmtrain.ops.build`)"
             return False

@@ -348,9 +348,11 @@ hipError_t launch_gemm_pp(const void* x, int ldx, const void* w, int ldw, const 
   if (epi == 3 && (delta == nullptr || T <= 0 || M % T != 0 || N % 64 != 0)) return hipErrorInvalidValue;
   const int tiles_m = (M + gpp::TW - 1) / gpp::TW, tiles_n = (N + gpp::TW - 1) / gpp::TW;
   const int nwg = tiles_m * tiles_n;
+  // fill placement (A/B knob LLMT_GPP_FILL=3: fills inside the MFMA segment; 1 measured equal or
+  // faster on 8 of the 9 shapes, profiles/r4/gemm_pp/op_times_vs_hipblaslt.txt)
   static const int fill = [] {
     const char* e = std::getenv("LLMT_GPP_FILL");
-    return e != nullptr && std::atoi(e) == 1 ? 1 : 3;
+    return e != nullptr && std::atoi(e) == 3 ? 3 : 1;
   }();
 #define LLMT_GPP_LAUNCH(E, F, KN)                                                                                 \
   hipLaunchKernelGGL((gpp::gemm_pp_kernel<E, F, KN>), dim3(nwg), dim3(gpp::kThreads), 0, stream,                   \

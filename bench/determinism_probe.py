@@ -99,7 +99,7 @@ def main() -> int:
     torch.cuda.synchronize()
     print(json.dumps({
         "summary": True, "steps": args.steps, "reps": args.reps, "micro_batch": args.micro_batch,
-        "mismatches": bad_total, "wgrad_stream": os.environ.get("LLMTRAIN_WGRAD_STREAM", "1"),
+        "mismatches": bad_total, "wgrad_stream": os.environ.get("LLMTRAIN_WGRAD_STREAM", "0"),
         "tuned_table": bool(getattr(trainer, "tuned_gemms", False)),
         "master_checksum": float(store.master.double().sum()),
     }), flush=True)
@@ -141,7 +141,7 @@ def compare_runs(cfg, args: argparse.Namespace) -> int:  # type: ignore[no-untyp
               flush=True)
     print(json.dumps({"summary": True, "mode": "runs", "runs": args.runs, "steps": args.steps,
                       "micro_batch": args.micro_batch, "runs_differing": bad,
-                      "wgrad_stream": os.environ.get("LLMTRAIN_WGRAD_STREAM", "1")}), flush=True)
+                      "wgrad_stream": os.environ.get("LLMTRAIN_WGRAD_STREAM", "0")}), flush=True)
     return 1 if bad else 0
 
 

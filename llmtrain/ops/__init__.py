@@ -54,7 +54,7 @@ def _on_gpu(t: torch.Tensor) -> bool:
     return t.device.type == "cuda"
 
 
-_POLICY = {"gemm_all_ours": False, "single_stream": False}
+_POLICY = {"gemm_all_ours": False, "single_stream": False, "deterministic": False}
 
 # How run.deterministic keeps the step bitwise reproducible (LLMTRAIN_DET_SCHEDULE overrides):
 #  * "serial": the weight-gradient GEMMs run on the main stream (no side stream), the forward / dX
@@ -79,6 +79,7 @@ def set_deterministic(on: bool, schedule: str | None = None) -> bool:
         raise ValueError(f"deterministic schedule must be one of {DET_SCHEDULES}, not {schedule!r}")
     _POLICY["gemm_all_ours"] = bool(on) and schedule == "ours"
     _POLICY["single_stream"] = bool(on) and schedule == "serial"
+    _POLICY["deterministic"] = bool(on)
     if not _ext.load():
         return False
     prev = bool(torch.ops.llmtrain_hip.get_deterministic())
@@ -275,11 +276,11 @@ FGEMM_ANY_SIZE = frozenset(os.environ.get("LLMTRAIN_FGEMM_ANY", "dx_gelu,dx_attn
 _WARNED: set[str] = set()
 
 
-def _det_fallback(what: str) -> None:
+def _det_fallback(what: str, always: bool = False) -> None:
     """Deterministic mode promises every forward / dX GEMM on the hand-written kernel; a shape it
     cannot take runs on hipBLASLt, whose Stream-K solutions are not run-to-run reproducible beside
     the weight-gradient side stream.  Say so once per distinct case instead of failing silently."""
-    if _POLICY["gemm_all_ours"] and what not in _WARNED:
+    if (_POLICY["gemm_all_ours"] or (always and _POLICY["deterministic"])) and what not in _WARNED:
         _WARNED.add(what)
         import warnings
 
@@ -382,7 +383,7 @@ def linear_fwd(x, w, bias=None):
     if _gpp_ok("fwd", x, w, bias):
         return hip_ops().gemm_pp(x, w, bias, 0)[0]
     if (_on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x, x.shape[1], w.shape[0], w, bias, op="fwd")
-            and (_POLICY["gemm_all_ours"] or bias is None
+            and (_POLICY["deterministic"] or bias is None
                  or not _library_tuned_bias_gemm(x.shape[0], w.shape[0], x.shape[1]))):
         return _gemm_rows(x, w, False, 0, bias)[0]
     return torch.mm(x, w.t()) if bias is None else torch.addmm(bias, x, w.t())
@@ -429,9 +430,17 @@ def head_logits(h, w):
 
 def head_dx(dlogits, w):
     """``dh = dlogits @ w`` (LM-head data gradient, ``w [Vp, d]``), row-chunked like
-    :func:`head_logits` on our kernel."""
-    if not (_on_gpu(dlogits) and _POLICY["gemm_all_ours"] and dlogits.dtype == torch.bfloat16
-            and _fgemm_ok(dlogits, dlogits.shape[1], w.shape[1], w)):
+    :func:`head_logits` on our kernel.  Deterministic mode always takes our kernel here: this is the
+    step's only GEMM with a 50304-deep reduction, where the library picks split / Stream-K
+    solutions whose partial sums combine in completion order — the one run-to-run difference left
+    in the serial schedule (bench/determinism_probe.py at micro-batch 8: the gradients first differ
+    at ln_f, the head dX's output)."""
+    k, n = dlogits.shape[1], w.shape[1]
+    if not (_on_gpu(dlogits) and _POLICY["deterministic"] and dlogits.dtype == torch.bfloat16
+            and k % 64 == 0 and k >= 256 and n % 8 == 0  # the size cap does not apply: row chunks
+            and dlogits.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and dlogits.stride(1) == 1):
+        if _on_gpu(dlogits) and _POLICY["deterministic"]:
+            _det_fallback(f"LM-head dX K={k} N={n}", always=True)
         return torch.mm(dlogits, w)
     out = torch.empty(dlogits.shape[0], w.shape[1], dtype=dlogits.dtype, device=dlogits.device)
     for r0 in range(0, dlogits.shape[0], _HEAD_ROWS):

@@ -4,7 +4,7 @@
     python bench/gemm_pp.py time [--tokens M] [--only pp,blas,fused]   # forward and dX shapes
 
 Each timing line: kernel, shape, ms (median of 20), TFLOP/s on the 2*M*N*K GEMM FLOPs.
-LLMT_GPP_FILL=1 selects the fills-in-LOAD schedule (default 3: fills inside the MFMA segment).
+LLMT_GPP_FILL=3 selects the fills-inside-MFMA schedule (default 1: fills in the LOAD segment).
 """
 
 from __future__ import annotations

@@ -99,7 +99,10 @@ k8s-cluster-delete: k8s-kind-delete
 k8s-kind-load: k8s-build
 	kind load docker-image llmtrain-mi355x:dev --name llmtrain
 
-k8s-full: k8s-cluster k8s-kind-load k8s-train k8s-logs
+# kind has no AMD GPU device plugin: the reference-named end-to-end target runs the CPU Job on kind
+# (k8s/kind/*), exactly like the reference's CPU-only k8s-full; the GPU Job (k8s-train) needs a
+# cluster with the AMD device plugin and MI355X nodes
+k8s-full: k8s-cluster k8s-kind-smoke k8s-logs
 
 k8s-kind-smoke: k8s-build
 	kind load docker-image llmtrain-mi355x:dev --name llmtrain

@@ -52,9 +52,7 @@ def gemm(M: int = 32768, only: str = "") -> list[dict]:
             "dW mm bf16": lambda: torch.mm(dy.t(), x),
             "dW mm bf16 + add": lambda: acc.add_(torch.mm(dy.t(), x)),
             "dW^T mm bf16 (x^T dy)": lambda: torch.mm(x.t(), dy),
-            "dW llmtrain wgrad auto": lambda: torch.ops.llmtrain_hip.wgrad_gemm(dy, x, acc, 0, 0),
-            "dW llmtrain wgrad tile128": lambda: torch.ops.llmtrain_hip.wgrad_gemm(dy, x, acc, 0, 128),
-            "dW llmtrain wgrad tile256": lambda: torch.ops.llmtrain_hip.wgrad_gemm(dy, x, acc, 0, 256),
+            "dW llmtrain wgrad": lambda: torch.ops.llmtrain_hip.wgrad_gemm_pp(dy, x, acc, None, 0, -1),
             "dW hipblaslt bmm split8 + sum": lambda: acc.add_(
                 torch.bmm(dy.view(8, M // 8, N).transpose(1, 2), x.view(8, M // 8, K)).float().sum(0)
             ),
@@ -143,57 +141,6 @@ def fgemm_one(K: int, N: int, epi: int = 0, b_kn: bool = False, M: int = 65536, 
                       "TFLOPs": round(2.0 * M * K * N / ms / 1e9, 1)}), flush=True)
 
 
-def fgemm_ab(M: int = 131072, variants: str = "LLMT_FGEMM_DEBUG=0", rounds: int = 3) -> None:
-    """Interleaved in-process A/B of fused-GEMM variants selected per launch by environment
-    (``NAME=VALUE`` each, read by csrc/gemm_fused.hip at every launch) on every GPT-2 124M
-    forward/dX shape (and the epilogue variants), vs hipBLASLt."""
-    import os
-
-    from llmtrain.ops import _ext
-
-    _ext.require()
-    ops = torch.ops.llmtrain_hip
-    dev = torch.device("cuda")
-    shapes = {"qkv": (768, 2304), "out": (768, 768), "fc": (768, 3072), "proj": (3072, 768)}
-    for name, (K, N) in shapes.items():
-        x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
-        w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) / K**0.5
-        dy = torch.randn(M, N, device=dev, dtype=torch.bfloat16)
-        bias = torch.randn(N, device=dev, dtype=torch.bfloat16)
-        cases = {
-            "fwd": (lambda: ops.gemm_fused(x, w, False, 0, bias), lambda: torch.addmm(bias, x, w.t())),
-            "dX": (lambda: ops.gemm_fused(dy, w, True, 0), lambda: torch.mm(dy, w)),
-        }
-        if name == "proj":  # the MLP projection dX with GELU backward + fc-bias grad (epilogue 2)
-            u = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
-            dbk = torch.zeros(K, device=dev)
-            cases["dX+dgelu"] = (lambda: ops.gemm_fused(dy, w, True, 2, None, u, dbk),
-                                 lambda: ops.gelu_bwd(torch.mm(dy, w), u, dbk))
-        if name == "out":  # the attention out-proj dX with delta + V-bias (epilogue 3)
-            att = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
-            dbk2 = torch.zeros(K, device=dev)
-            cases["dX+delta"] = (lambda: ops.gemm_fused(dy, w, True, 3, None, att, dbk2, 1024),
-                                 lambda: torch.mm(dy, w))
-        if name == "fc":
-            cases["fwd+gelu"] = (lambda: ops.gemm_fused(x, w, False, 1, bias),
-                                 lambda: ops.gelu_fwd(torch.addmm(bias, x, w.t())))
-        flops = 2.0 * M * K * N
-        for cname, (ours, lib) in cases.items():
-            res: dict[str, list[float]] = {}
-            for _ in range(rounds):
-                for v in variants.split(","):
-                    key, _, val = v.partition("=")
-                    os.environ[key] = val
-                    res.setdefault(f"llmt[{v}]", []).append(timeit(ours, iters=10, warmup=2))
-                    os.environ.pop(key, None)
-                res.setdefault("hipblaslt", []).append(timeit(lib, iters=10, warmup=2))
-            row = {"gemm": name, "case": cname, "M": M}
-            for k, v in res.items():
-                ms = sorted(v)[len(v) // 2]
-                row[k] = {"ms": round(ms, 4), "TF": round(flops / ms / 1e9, 1)}
-            print(json.dumps(row), flush=True)
-
-
 def ln(M: int = 65536, d: int = 768) -> None:
     """LayerNorm forward (+residual add) and backward at the engine's call shapes; GB/s moved."""
     from llmtrain.ops import _ext
@@ -269,9 +216,6 @@ if __name__ == "__main__":
     if what == "fgemm1":  # K N epi b_kn
         fgemm_one(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5] == "1",
                   M=int(sys.argv[6]) if len(sys.argv) > 6 else 65536)
-    if what == "fgemm_ab":  # M variants
-        fgemm_ab(int(sys.argv[2]) if len(sys.argv) > 2 else 131072,
-                 sys.argv[3] if len(sys.argv) > 3 else "LLMT_FGEMM_DEBUG=0")
     if what == "fgemm":
         fgemm(int(sys.argv[2]) if len(sys.argv) > 2 else 65536)
     if what == "fgemm_head":  # LM-head shapes (K 768 fwd, K 50304 dX)

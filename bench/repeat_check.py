@@ -83,10 +83,10 @@ def main() -> None:
             (f32z(d), f32z(d), f32z(d)), lambda a: hip.layernorm_bwd(dout, xs, mu, rs, w_ln, dres, a[0], a[1], None, True, a[2])
         ),
         "wgrad fc (det slabs)": lambda: _with(
-            torch.zeros(4 * d, d, device="cuda"), lambda c: hip.wgrad_gemm(u, x768, c, 0, 0, -1)
+            torch.zeros(4 * d, d, device="cuda"), lambda c: hip.wgrad_gemm_pp(u, x768, c, None, 0, -1)
         ),
         "wgrad qkv (det slabs)": lambda: _with(
-            torch.zeros(3 * d, d, device="cuda"), lambda c: hip.wgrad_gemm(x2304, x768, c, 0, 0, -1)
+            torch.zeros(3 * d, d, device="cuda"), lambda c: hip.wgrad_gemm_pp(x2304, x768, c, None, 0, -1)
         ),
     }
 

@@ -1,8 +1,7 @@
-"""Weight-gradient GEMM: ping-pong kernel (csrc/gemm_wgrad_pp.hip) vs the round-3 kernels.
+"""Weight-gradient GEMM (csrc/gemm_wgrad_pp.hip): numerics and per-shape timing.
 
     python bench/wgrad_pp.py check            # numerics vs fp32 (every shape, bias, strided dy)
     python bench/wgrad_pp.py time [--tokens M] [--model gpt2-124m|gpt2-xl|head]
-    LLMT_WPP_SKEL=9 python bench/wgrad_pp.py probe --gemm qkv   # cycles per phase part
 
 Each timing line: kernel, shape, ms (median of 20), TFLOP/s on the 2*M*N*K GEMM FLOPs.
 """
@@ -82,8 +81,6 @@ def time_shapes(model: str, M: int, only: str = "") -> None:
         bias = torch.zeros(N, device="cuda")
         flops = 2.0 * M * N * K
         variants = {
-            "r3_tile256": lambda: ops.wgrad_gemm(dy, x, acc, 0, 256, 0),
-            "r3_pipe": lambda: ops.wgrad_gemm(dy, x, acc, 0, 256, 4),
             "pp_auto": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, -1),
             "pp_slab": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, 0),
             "pp_atomic": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, 2),
@@ -105,43 +102,15 @@ def one(gemm: str, variant: str, M: int, reps: int) -> None:
     dy = torch.randn(M, lda, device="cuda", dtype=torch.bfloat16)[:, :N]
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     acc = torch.zeros(N, K, device="cuda")
-    fn = {"r3_tile256": lambda: ops.wgrad_gemm(dy, x, acc, 0, 256, 0),
-          "r3_pipe": lambda: ops.wgrad_gemm(dy, x, acc, 0, 256, 4),
-          "pp": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, -1)}[variant]
+    fn = {"pp": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, -1)}[variant]
     for _ in range(reps):
         fn()
     torch.cuda.synchronize()
 
 
-def probe(gemm: str, M: int) -> None:
-    """Per-phase cycle split of the ping-pong kernel (needs LLMT_WPP_SKEL=9 in the environment): mean
-    cycles per phase of each part, for the X waves (0-3) and the Y waves (4-7) of workgroups 0-255."""
-    ops = _ops()
-    N, K = {**SHAPES["gpt2-124m"], **SHAPES["head"]}[gemm]
-    lda = 50304 if N == 50257 else N
-    dy = torch.randn(M, lda, device="cuda", dtype=torch.bfloat16)[:, :N]
-    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
-    acc = torch.zeros(N, K, device="cuda")
-    buf = torch.zeros(256 * 64, dtype=torch.int64, device="cuda")
-    ops.wgrad_pp_probe(buf)
-    for _ in range(3):
-        ops.wgrad_gemm_pp(dy, x, acc, None, 0, 0)
-    torch.cuda.synchronize()
-    ops.wgrad_pp_probe(torch.empty(0, device="cuda"))
-    v = buf.view(256, 8, 8)[:, :, :6].double()
-    nph = v[:, :, 5:6].clamp(min=1)
-    per = v[:, :, :5] / nph  # cycles per phase
-    names = ["reads", "writes+loads", "wait+barrierA", "mfma_issue", "barrierB"]
-    for grp, sl in (("X", slice(0, 4)), ("Y", slice(4, 8))):
-        m = per[:, sl].mean(dim=(0, 1))
-        print(json.dumps({"gemm": gemm, "M": M, "waves": grp, "phases": int(v[0, 0, 5].item()),
-                          **{n: round(m[i].item(), 1) for i, n in enumerate(names)},
-                          "total": round(m.sum().item(), 1)}), flush=True)
-
-
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["check", "time", "one", "probe"])
+    ap.add_argument("what", choices=["check", "time", "one"])
     ap.add_argument("--gemm", default="qkv")
     ap.add_argument("--variant", default="pp")
     ap.add_argument("--reps", type=int, default=10)
@@ -151,9 +120,6 @@ def main() -> int:
     args = ap.parse_args()
     if args.what == "check":
         return check()
-    if args.what == "probe":
-        probe(args.gemm, args.tokens)
-        return 0
     if args.what == "one":
         one(args.gemm, args.variant, args.tokens, args.reps)
         return 0

@@ -8,7 +8,6 @@
 // no extra pass over the gradients.  The update order matches torch.optim.AdamW exactly:
 //   p *= 1 - lr*wd;  m += (1-b1)(g-m);  v = b2 v + (1-b2) g^2;
 //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
-#include <cstdlib>
 
 #include "common.h"
 #include "kernels.h"
@@ -89,9 +88,10 @@ __device__ __forceinline__ void store_shadow(void* shadow, long i, float4_t p) {
   }
 }
 
-// Tiled variant (default; LLMT_ADAMW_TILED=0 restores the grid-stride kernel): one tile of 2 x 256 float4 groups per workgroup, all eight
-// loads of a thread issued before the first wait, no grid stride; the n % 4 tail stays with the
-// grid-stride kernel's scalar loop (launched as a second, tiny kernel when present).
+// Tiled variant (default; the grid-stride kernel takes sizes not a multiple of 4): one tile of
+// 2 x 256 float4 groups per workgroup, all eight loads of a thread issued before the first wait,
+// no grid stride; the n % 4 tail stays with the grid-stride kernel's scalar loop (launched as a
+// second, tiny kernel when present).
 template <bool SHADOW_BF16>
 __global__ __launch_bounds__(256) void adamw_tiled_kernel(float* __restrict__ param, const float* __restrict__ grad,
                                                           float* __restrict__ m, float* __restrict__ v,
@@ -156,14 +156,20 @@ constexpr int kSumsqThreads = 256;
 __global__ __launch_bounds__(kSumsqThreads) void sumsq_partial_kernel(const float* __restrict__ x, long n,
                                                                       float* __restrict__ partials) {
   __shared__ float scratch[kSumsqThreads / 64];
-  const long n4 = n >> 2;
   const long stride = (long)gridDim.x * blockDim.x;
   float acc = 0.f;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4_t a = reinterpret_cast<const float4_t*>(x)[i];
+  // x may start anywhere (a bucket view of the flat gradient buffer): scalar head up to the first
+  // 16-byte boundary, float4 body, scalar tail
+  const long head = min(n, (long)((4 - (((unsigned long)x >> 2) & 3)) & 3));
+  const long body4 = (n - head) >> 2;
+  const float4_t* xb = reinterpret_cast<const float4_t*>(x + head);
+  const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (long i = t0; i < body4; i += stride) {
+    float4_t a = xb[i];
     acc += a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3];
   }
-  for (long i = (n4 << 2) + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) acc += x[i] * x[i];
+  if (t0 < head) acc += x[t0] * x[t0];
+  for (long i = head + (body4 << 2) + t0; i < n; i += stride) acc += x[i] * x[i];
   acc = block_sum<kSumsqThreads / 64>(acc, scratch);
   if (threadIdx.x == 0) partials[blockIdx.x] = acc;
 }

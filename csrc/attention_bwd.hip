@@ -38,7 +38,6 @@
 //    (key padding) zeroes P of this lane's key when it is padded — one per-lane flag, because the
 //    key sits on the MFMA lane here (rows the forward marked dead have lse = +inf, so P = 0).
 
-#include <cstdlib>
 
 #include "attention_common.h"
 

@@ -32,7 +32,6 @@
 //    row whose keys so far are ALL masked keeps m = -inf: its exponent offset is taken as 0 then
 //    (P = exp2(-inf) = 0, no inf - inf), and the first real key rescales with alpha = 0; rows that
 //    never saw a real key are written as O = 0, lse = +inf.
-#include <cstdlib>
 
 #include "attention_common.h"
 
@@ -303,203 +302,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
   ATTN_PROBE(63);
 }
 
-
-// ---------------------------------------------------------------------------------------------
-// Ping-pong forward (hd 64, no dropout / key mask): 512-thread workgroups = 8 waves x 32 query rows
-// (a 256-row query block), 2 waves per SIMD.  Waves 0-3 ("X") and 4-7 ("Y") run one barrier
-// apart, so on every SIMD one wave's softmax (VALU: max, exp, sum, pack) runs beside its
-// partner's MFMAs (P V of the previous tile + S = K Q^T of the next), in alternating segments:
-//
-//     X: S(0) | sm(0)        | PV(0) S(1) | sm(1)      | PV(1) S(2) | ...
-//     Y: ---- | S(0)         | sm(0)      | PV(0) S(1) | sm(1)      | ...
-//
-// (the 4-wave kernel above relies on two independent workgroups per CU drifting into such an
-// overlap; here it is scheduled).  K/V tiles of 64 keys go through a 4-slot LDS ring (64 KiB),
-// register-staged, with ONE program for both halves: a wave writes tile t+2 in its softmax
-// segment of tile t (the slot of tile t-2, whose last reader, Y's P V, finished two segments
-// earlier) and loads tile t+4 into the freed registers in its MFMA segment; each wave's writes
-// land before the barrier that closes the segment.  Waves whose rows all precede a tile's keys
-// skip its compute but keep the barrier schedule.
-constexpr int kPPWaves = 8;
-constexpr int kPPQ = 32 * kPPWaves;  // 256 query rows per workgroup
-constexpr int kPPSlots = 4;
-
-__global__ __launch_bounds__(512, 1) void attn_fwd_pp_kernel(const bf16_raw* __restrict__ qkv,
-                                                            bf16_raw* __restrict__ out, float* __restrict__ lse,
-                                                            int T, int H, int nqb) {
-  __shared__ __attribute__((aligned(16))) bf16_raw smem[kPPSlots][2][kKBlk * kHD];  // [slot][K|V]
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wn = wave >> 2;
-  const int half = lane >> 5, col = lane & 31;
-  int bh, qrank;
-  chunked_dispatch(bh, qrank);
-  const int qb = nqb - 1 - qrank;
-  const int b = bh / H, h = bh - b * H;
-  const long row_stride = 3L * H * kHD;
-  const bf16_raw* base = qkv + (long)b * T * row_stride + (long)h * kHD;
-  const int q0w = qb * kPPQ + wave * 32;
-  const int q = q0w + col;
-  const int q_hi = min(q0w + 31, T - 1);
-
-  bf16x8 qf[4];
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) {
-    ushort8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (q < T) v = *reinterpret_cast<const ushort8_t*>(base + (long)q * row_stride + 16 * kk + 8 * half);
-    qf[kk] = __builtin_bit_cast(bf16x8, v);
-  }
-  const int kv_end = min(T, qb * kPPQ + kPPQ);
-  const int ntiles = (kv_end + kKBlk - 1) / kKBlk;
-  const int nt2 = (ntiles + 1) & ~1;  // iterations in pairs (register-set parity); the pad tile is idle
-
-  const __amdgpu_buffer_rsrc_t rkv = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)base, (short)0, (int)(((long)T - 1) * row_stride + 3 * kHD * H) * 2, 0x00020000);
-  // fill: thread t moves chunk (t & 7) of key row t >> 3 of the K and of the V tile
-  const int frow = threadIdx.x >> 3, fch = threadIdx.x & 7;
-  const int foff = tile_chunk_off(frow, fch);
-  u32x4 set0[2], set1[2];  // tile s lives in set s & 1 between its load and its LDS write
-  auto load_tile = [&](u32x4(&st)[2], int tile) {
-    const int off = (int)(((long)(tile * kKBlk + frow) * row_stride + fch * 8 + kHD * H) * 2);
-    st[0] = __builtin_amdgcn_raw_buffer_load_b128(rkv, off, 0, 0);
-    st[1] = __builtin_amdgcn_raw_buffer_load_b128(rkv, off + kHD * H * 2, 0, 0);
-  };
-  auto store_tile = [&](const u32x4(&st)[2], int tile) {
-    const int slot = tile & (kPPSlots - 1);
-    *reinterpret_cast<u32x4*>(&smem[slot][0][foff]) = st[0];
-    *reinterpret_cast<u32x4*>(&smem[slot][1][foff]) = st[1];
-  };
-  auto bar = [] { asm volatile("s_barrier" ::: "memory"); };
-  auto lds_bar = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-
-  f32x16 o[2];
-  o[0] = 0.f;
-  o[1] = 0.f;
-  float m_run = -INFINITY, l_run = 0.f;
-  const float c = 0.125f * 1.4426950408889634f;
-  f32x16 s[2];
-  bf16x8 pb[2][2];
-  auto active = [&](int t) { return t * kKBlk <= q_hi; };  // wave-uniform
-
-  auto compute_s = [&](int t) {  // S^T = K_t Q^T
-    const bf16_raw* kl = smem[t & (kPPSlots - 1)][0];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      s[kt] = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const bf16x8 a = lds_row_read(kl, kt * 32 + col, 2 * kk + half);
-        s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[kk], s[kt], 0, 0, 0);
-      }
-    }
-  };
-  auto compute_pv = [&](int t) {  // O^T += V_t^T P^T
-    const bf16_raw* vl = smem[t & (kPPSlots - 1)][1];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const bf16x8 va = lds_tr_read_operand(vl, kt * 32 + 16 * st + 4 * half, dt * 32, lane);
-          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb[kt][st], o[dt], 0, 0, 0);
-        }
-  };
-  auto softmax = [&](int t) {  // mask, online max / rescale, P = exp2, row sums, P packed to bf16
-    const int kbase = t * kKBlk;
-    if ((kbase + kKBlk - 1 > q0w) || (kbase + kKBlk > T)) {
-      const int lim = min(q, T - 1) - kbase - 4 * half;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[kt][r] = ((r & 3) + 8 * (r >> 2) + 32 * kt > lim) ? -INFINITY : s[kt][r];
-    }
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, s[kt][r]);
-    tmax = halves_max(tmax);
-    if (__builtin_amdgcn_ballot_w64((tmax - m_run) * c > 8.f) != 0) {  // lazy rescale (see above)
-      const float m_new = fmaxf(m_run, tmax);
-      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
-      l_run *= alpha;
-      o[0] *= alpha;
-      o[1] *= alpha;
-      m_run = m_new;
-    }
-    const f32x2 cc = {c, c}, nmc = {-m_run * c, -m_run * c};
-    f32x2 ps = {0.f, 0.f};
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const f32x2 x = {s[kt][r], s[kt][r + 1]};
-        const f32x2 y = __builtin_elementwise_fma(x, cc, nmc);
-        const f32x2 e = {__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
-        s[kt][r] = e[0];
-        s[kt][r + 1] = e[1];
-        ps += e;
-      }
-    l_run += ps[0] + ps[1];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int st = 0; st < 2; ++st) pb[kt][st] = pack_acc8(s[kt], st);
-  };
-
-  // prologue: tiles 0, 1 in LDS, tiles 2, 3 loading; X computes S(0), Y joins one barrier later
-  load_tile(set0, 0);
-  load_tile(set1, 1);
-  store_tile(set0, 0);
-  store_tile(set1, 1);
-  load_tile(set0, 2);
-  load_tile(set1, 3);
-  lds_bar();
-  if (wn == 1) bar();
-  __builtin_amdgcn_s_setprio(1);
-  if (active(0)) compute_s(0);
-  __builtin_amdgcn_s_setprio(0);
-  bar();
-  // one tile: softmax segment (+ LDS write of tile t+2 from set A), then MFMA segment (P V of t,
-  // S of t+1, + loads of tile t+4 into set A)
-  auto step = [&](int t, u32x4(&A)[2]) {
-    const bool act = active(t), act1 = active(t + 1);
-    if (act) softmax(t);
-    store_tile(A, t + 2);
-    lds_bar();
-    __builtin_amdgcn_s_setprio(1);
-    if (act) compute_pv(t);
-    if (act1) compute_s(t + 1);
-    __builtin_amdgcn_s_setprio(0);
-    load_tile(A, t + 4);
-    bar();
-  };
-  for (int t = 0; t < nt2; t += 2) {
-    step(t, set0);
-    step(t + 1, set1);
-  }
-  if (wn == 0) bar();  // X matches Y's extra barrier
-
-  l_run = halves_sum(l_run);
-  if (q < T) {
-    const float inv_l = 1.f / l_run;
-    bf16_raw* dst = out + ((long)b * T + q) * H * kHD + (long)h * kHD;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        ushort4_t v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = f2bf(o[dt][4 * g + i] * inv_l);
-        *reinterpret_cast<ushort4_t*>(dst + dt * 32 + 8 * g + 4 * half) = v;
-      }
-    }
-    if (half == 0) lse[((long)b * H + h) * T + q] = (m_run * c + log2f(l_run)) * 0.6931471805599453f;
-  }
-}
-
 }  // namespace attn
 
 #ifdef LLMT_ATTN_PROBE
@@ -533,17 +335,6 @@ hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, const AttnDim
       case 4: launch_fwd_variant<true, false, false, 2>(grid, stream, q, o, lse, d, nqb, dropout); break;
       default: launch_fwd_variant<true, true, false, 2>(grid, stream, q, o, lse, d, nqb, dropout); break;
     }
-    return hipGetLastError();
-  }
-  // the scheduled ping-pong body for the common case (LLMT_ATTN_FWD_PP=1; A/B knob)
-  static const bool pp = [] {
-    const char* e = std::getenv("LLMT_ATTN_FWD_PP");
-    return e != nullptr && std::atoi(e) != 0;
-  }();
-  if (variant == 0 && pp) {
-    const int nqb_pp = (d.T + attn::kPPQ - 1) / attn::kPPQ;
-    hipLaunchKernelGGL(attn::attn_fwd_pp_kernel, dim3(d.B * d.H, nqb_pp), dim3(512), 0, stream, q, o, lse, d.T, d.H,
-                       nqb_pp);
     return hipGetLastError();
   }
   switch (variant) {

@@ -480,26 +480,6 @@ Tensor dropout_mask(int64_t n, double p, int64_t seed, const Tensor& like) {
 }
 
 // ---- weight-gradient GEMM --------------------------------------------------------------------
-void wgrad_gemm(const Tensor& dy, const Tensor& x, Tensor c, int64_t split, int64_t tile, int64_t pipe) {
-  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && c.is_cuda(), "wgrad_gemm: GPU tensors required");
-  check_dtype(dy, at::kBFloat16, "dy");
-  check_dtype(x, at::kBFloat16, "x");
-  check_dtype(c, at::kFloat, "c");
-  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && c.dim() == 2, "wgrad_gemm: 2D operands");
-  TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1 && c.stride(1) == 1, "wgrad_gemm: unit inner stride");
-  const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
-  TORCH_CHECK(x.size(0) == M && c.size(0) == N && c.size(1) == K, "wgrad_gemm: shape mismatch");
-  at::hip::HIPGuardMasqueradingAsCUDA guard(c.device());
-  // deterministic mode: per-M-chunk partial slabs, reduced in a fixed order (no split-K atomics)
-  const long det = llmt::wgrad_gemm_det_ws_floats((int)dy.stride(0), (int)x.stride(0), (int)M, (int)N, (int)K,
-                                                  (int)split, (int)tile);
-  Tensor ws = workspace(c, det);
-  check_hip(llmt::launch_wgrad_gemm(dy.data_ptr(), (int)dy.stride(0), x.data_ptr(), (int)x.stride(0),
-                                    c.data_ptr<float>(), (int)c.stride(0), (int)M, (int)N, (int)K, (int)split,
-                                    (int)tile, cur_stream(), det > 0 ? ws.data_ptr<float>() : nullptr, (int)pipe),
-            "wgrad_gemm");
-}
-
 // dst[N, K] (fp32) += dy[M, N]^T x[M, K], and bias[N] += colsum(dy) when given (ping-pong kernel)
 void wgrad_gemm_pp(const Tensor& dy, const Tensor& x, Tensor c, const c10::optional<Tensor>& bias, int64_t split,
                    int64_t mode) {
@@ -528,15 +508,6 @@ void wgrad_gemm_pp(const Tensor& dy, const Tensor& x, Tensor c, const c10::optio
                                   c.data_ptr<float>(), (int)c.stride(0), (int)M, (int)N, (int)K, (int)split, (int)mode,
                                   wsf > 0 ? ws.data_ptr<float>() : nullptr, bptr, cur_stream()),
             "wgrad_gemm_pp");
-}
-
-// timing probe of the ping-pong kernel (LLMT_WPP_SKEL=9): buf = int64 [256 * 8 * 8]
-// (an empty tensor clears it)
-void wgrad_pp_probe(const Tensor& buf) {
-  check_gpu(buf, "buf");
-  TORCH_CHECK(buf.numel() == 0 || (buf.scalar_type() == at::kLong && buf.numel() >= 256 * 64),
-              "wgrad_pp_probe: int64[16384]");
-  check_hip(llmt::wgrad_pp_set_probe(buf.numel() ? buf.data_ptr() : nullptr), "wgrad_pp_probe");
 }
 
 // ---- fused forward / dX GEMM ------------------------------------------------------------------
@@ -614,58 +585,6 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tens
   Tensor ws = workspace(a, g.dbias != nullptr ? llmt::gemm_fused_ws_floats((int)M, (int)N) : 0);
   g.ws = ws.data_ptr<float>();
   if (M > 0) check_hip(llmt::launch_gemm_fused(g, cur_stream()), "gemm_fused");
-  return {out, out2};
-}
-
-// ---- ping-pong GEMM: x @ w^T + bias (gelu of it for epi 1); kn: x @ w (epi 2: * gelu'(u)) -------
-std::tuple<Tensor, c10::optional<Tensor>> gemm_pp(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
-                                                  int64_t epi, bool kn, const c10::optional<Tensor>& u, int64_t seq_len) {
-  check_gpu(x, "x");
-  check_gpu(w, "w");
-  check_dtype(x, at::kBFloat16, "x");
-  check_dtype(w, at::kBFloat16, "w");
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1, "gemm_pp: 2D row-major operands");
-  const int64_t M = x.size(0), K = x.size(1), N = kn ? w.size(1) : w.size(0);
-  TORCH_CHECK((kn ? w.size(0) : w.size(1)) == K, "gemm_pp: inner dimensions differ");
-  TORCH_CHECK(kn ? (epi == 0 || epi == 2 || epi == 3) : (epi == 0 || epi == 1),
-              "gemm_pp: epi 0 / 1 (forward) or 0 / 2 / 3 (kn)");
-  TORCH_CHECK(llmt::gemm_pp_supported((int)M, (int)N, (int)K, (int)x.stride(0), (int)w.stride(0), (int)N, kn),
-              "gemm_pp: needs K % 64 == 0, N % 8 == 0, 16-byte row strides");
-  TORCH_CHECK((uintptr_t)x.data_ptr() % 16 == 0 && (uintptr_t)w.data_ptr() % 16 == 0, "gemm_pp: 16-byte aligned operands");
-  const void* bptr = nullptr;
-  if (bias.has_value()) {
-    TORCH_CHECK(!kn, "gemm_pp: no bias on the kn path");
-    check_gpu(*bias, "bias");
-    check_dtype(*bias, at::kBFloat16, "bias");
-    TORCH_CHECK(bias->numel() == N && (uintptr_t)bias->data_ptr() % 8 == 0, "gemm_pp: bias [N], 8-byte aligned");
-    bptr = bias->data_ptr();
-  }
-  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  Tensor out = at::empty({M, N}, x.options());
-  c10::optional<Tensor> out2;
-  void* c2 = nullptr;
-  if (epi == 1) {
-    out2 = at::empty({M, N}, x.options());
-    c2 = out2->data_ptr();
-  }
-  float* dptr = nullptr;
-  if (epi == 3) {
-    TORCH_CHECK(seq_len > 0 && M % seq_len == 0 && N % 64 == 0, "gemm_pp: epi 3 needs seq_len | M, 64 | N");
-    out2 = at::empty({M / seq_len, N / 64, seq_len}, x.options().dtype(at::kFloat));
-    dptr = out2->data_ptr<float>();
-  }
-  if (epi >= 2) {
-    TORCH_CHECK(u.has_value(), "gemm_pp: epi 2 / 3 needs u");
-    check_gpu(*u, "u");
-    check_dtype(*u, at::kBFloat16, "u");
-    TORCH_CHECK(u->dim() == 2 && u->size(0) == M && u->size(1) == N && u->is_contiguous(), "gemm_pp: u must be [M, N]");
-    c2 = u->data_ptr();
-  }
-  if (M > 0)
-    check_hip(llmt::launch_gemm_pp(x.data_ptr(), (int)x.stride(0), w.data_ptr(), (int)w.stride(0), bptr,
-                                   out.data_ptr(), c2, (int)N, (int)M, (int)N, (int)K, (int)epi, kn, dptr,
-                                   (int)seq_len, cur_stream()),
-              "gemm_pp");
   return {out, out2};
 }
 
@@ -771,10 +690,7 @@ TORCH_LIBRARY(llmtrain_hip, m) {
   m.def("set_deterministic(bool on) -> ()", &set_deterministic);  // catch-all: no tensor arguments
   m.def("get_deterministic() -> bool", &get_deterministic);
   m.def("set_dropout_seed_offset(Tensor? word) -> ()", &set_dropout_seed_offset);
-  m.def("wgrad_gemm(Tensor dy, Tensor x, Tensor(a!) c, int split=0, int tile=0, int pipe=-1) -> ()");
-  m.def("wgrad_pp_probe(Tensor buf) -> ()");
   m.def("wgrad_gemm_pp(Tensor dy, Tensor x, Tensor(a!) c, Tensor(b!)? bias=None, int split=0, int mode=-1) -> ()");
-  m.def("gemm_pp(Tensor x, Tensor w, Tensor? bias=None, int epi=0, bool kn=False, Tensor? u=None, int seq_len=0) -> (Tensor, Tensor?)");
   m.def("gemm_fused(Tensor a, Tensor b, bool b_kn, int epilogue, Tensor? bias=None, Tensor? u=None,"
         " Tensor(a!)? dbias=None, int seq_len=0) -> (Tensor, Tensor?)");
   m.def("sumsq(Tensor x) -> Tensor");
@@ -800,11 +716,8 @@ TORCH_LIBRARY_IMPL(llmtrain_hip, CUDA, m) {
   m.impl("attn_fwd", &attn_fwd);
   m.impl("attn_bwd", &attn_bwd);
   m.impl("dropout_mask", &dropout_mask);
-  m.impl("wgrad_gemm", &wgrad_gemm);
   m.impl("wgrad_gemm_pp", &wgrad_gemm_pp);
-  m.impl("wgrad_pp_probe", &wgrad_pp_probe);
   m.impl("gemm_fused", &gemm_fused);
-  m.impl("gemm_pp", &gemm_pp);
   m.impl("sumsq", &sumsq);
   m.impl("adamw_flat", &adamw_flat);
 }

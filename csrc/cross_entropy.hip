@@ -8,7 +8,6 @@
 //     dlogits = (softmax(z) - onehot(label)) * row_weight[row]      (0 for padded columns)
 // so the backward never touches the logits as logits again.  At GPT-2 vocab this is one read
 // and one write of 100 KB per row, i.e. HBM-bound at ~2 * M * Vp * 2 bytes.
-#include <cstdlib>
 
 #include "common.h"
 #include "kernels.h"

@@ -4,7 +4,6 @@
 //
 // Reference call sites: models/gpt.py:94-95/:102-103 (nn.GELU, exact erf), :176-179 (token and
 // position embeddings; gradient of the tied [V, d] table), Linear bias gradients.
-#include <cstdlib>
 
 #include "common.h"
 #include "kernels.h"

@@ -39,7 +39,6 @@
 //    whole 128-byte row segments per wave instruction, with buffer stores (out-of-range lanes get
 //    an offset past the descriptor, so the store count is branch-free and known: the counted
 //    waits after an epilogue rely on it); the tile's bias rides with its last K stage by LDS-DMA.
-#include <cstdlib>
 
 #include "common.h"
 #include "gemm_common.h"
@@ -218,7 +217,6 @@ struct Args {
   // 0.771; at M = 32768 mixed (qkv fwd 0.120 -> 0.133), so the rule is tied to the tile order's
   // (profiles/r3/nt/)
   int nt;
-  int debug;
 };
 
 template <bool NN, int EPI>
@@ -306,8 +304,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
     const int kk = is_s * BK;
     const int soa = (is_m0 * p.lda + kk) * 2;
     const int sob = NN ? (kk * p.ldb + is_n0) * 2 : (is_n0 * p.ldb + kk) * 2;
-    if (!(p.debug & 1))  // debug bit 0: skip the operand DMA (times the compute skeleton alone)
-      dma_stage(slot + wave * kDmaA * 1024, slot + kAElems * 2 + wave * kDmaB * 1024, va, vb, ra, rb, soa, sob);
+    dma_stage(slot + wave * kDmaA * 1024, slot + kAElems * 2 + wave * kDmaB * 1024, va, vb, ra, rb, soa, sob);
     if (kBiasDma && is_s == nst - 1) {
       // the tile's bias (this wave's 128 columns, bf16) rides with its last K stage into the head
       // of the wave's epilogue staging image: landed by that stage's wait, read before staging
@@ -594,10 +591,6 @@ hipError_t launch_gemm_fused(const GemmFusedArgs& g, hipStream_t stream) {
   a.ntiles = a.tiles_m * a.tiles_n;
   const int ncu = gemm::cu_count();
   a.nwg = a.ntiles < ncu ? a.ntiles : ncu;  // persistent: one workgroup per CU
-  // LLMT_FGEMM_DEBUG=1 (timing runs only, wrong results): no operand DMA — the compute skeleton
-  // alone; read per launch so one process can interleave it with the real kernel
-  const char* dbg = std::getenv("LLMT_FGEMM_DEBUG");
-  a.debug = dbg ? std::atoi(dbg) : 0;
   // at large M one band spans all of N: see tile_origin
   a.band = a.tiles_m >= kWideM || kBand >= a.tiles_n ? a.tiles_n : kBand;
   a.nt = a.tiles_m >= kWideM ? 1 : 0;

@@ -16,13 +16,13 @@
 // v_mfma_f32_16x16x32_bf16 accumulators (128 AGPRs).  The 16x16x32 shape is chosen over 32x32x16
 // at equal LDS traffic because the chip holds a higher clock on it (MI355X_MICROARCH, DVFS item 7).
 //
-// Stages of 32 reduction rows (one MFMA k-step) stream through a 4-slot LDS ring (4 x 32 KiB):
-//  * fills by `buffer_load_dwordx4 ... lds` (4 x 1 KiB per wave per stage); the buffer descriptor
-//    ends at the workgroup's row chunk, so rows past it read as zero;
-//  * LOAD(p) reads stage p, issues stage p+3 into the slot of stage p-1, then waits for its own
-//    reads (lgkmcnt(0)) and for stage p+1's fill (counted vmcnt) BEFORE the barrier: every wave has
-//    finished reading stage p-1 at the barrier that precedes any LOAD(p), so that slot is free,
-//    and stage p+1 has landed everywhere before any wave reads it;
+// Stages of 32 reduction rows (one MFMA k-step) stream through a 2-slot LDS ring (2 x 32 KiB):
+//  * register-staged fills (4 x 16 bytes per lane and stage); the buffer descriptor of a stage ends
+//    at the workgroup's row chunk, so rows past it read as zero;
+//  * LOAD(p) reads stage p's fragments, writes stage p+1 (loaded two phases earlier) into the other
+//    slot and loads stage p+3, then waits for its own LDS operations (lgkmcnt(0)) BEFORE the
+//    barrier: every wave finished reading stage p-1 (the other slot) at the barrier that precedes
+//    any LOAD(p), and stage p+1 has landed everywhere before any wave reads it;
 //  * both operands have the reduction index running down their rows, so fragments are read with
 //    ds_read_b64_tr_b16 (two per fragment: k rows 8g..8g+3 and 8g+4..8g+7); the 32-byte column
 //    segments of each 512-byte LDS row are XOR-swizzled by f(row) = (row & 3) | ((row >> 3) & 1) << 2,
@@ -43,8 +43,6 @@
 // Replaces the autograd weight (and bias) gradients of every nn.Linear of the reference
 // (models/gpt.py:27-29, 94-96, 184 via loss.backward() at training/trainer.py:386-387).
 #include <algorithm>
-#include <cstdlib>
-#include <string>
 
 #include "common.h"
 #include "gemm_common.h"
@@ -61,17 +59,11 @@ constexpr int TW = 256;        // tile edge
 constexpr int ROWB = TW * 2;   // LDS bytes per image row
 constexpr int IMG = BR * ROWB; // 16 KiB per operand per stage
 constexpr int SLOT = 2 * IMG;  // 32 KiB
-constexpr int NS_MAX = 5;      // ring slots (4 or 5: template parameter NSL)
 constexpr int FA = 8, FB = 4;  // 16-wide fragments per wave: 128 (n) x 64 (k)
 constexpr int NACC = FA * FB;
 constexpr int SLAB_FLOATS = TW * TW;  // one tile's partial
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
-
-// Timing probe (SKEL 9, LLMT_WPP_SKEL=9, bench/wgrad_pp.py probe): per wave, the shader-clock
-// cycles spent in each part of a phase summed over the phases, stored by workgroups < 256
-// as probe[(wg * 8 + wave) * 8 + part]
-__device__ unsigned long long* g_wpp_probe = nullptr;
 
 __device__ __forceinline__ int swz_f(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
 
@@ -80,17 +72,6 @@ __device__ __forceinline__ bf16x8 tr_read(unsigned addr) {
   const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(unsigned long)(addr + 4 * ROWB));
   const short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, v);
-}
-
-// own LDS reads done and at most n (0, 2, 4, 6, 8) younger fill ops outstanding, then the barrier
-__device__ __forceinline__ void wait_fill_barrier(int n) {
-  if (n >= 12) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if (n >= 10) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if (n >= 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if (n >= 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 __device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
@@ -106,25 +87,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, in
   return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long)hi << 32) | lo), (short)0, n, 0x00020000);
 }
 
-// PLACE: where a wave issues its 4 fill ops of stage st+3 — 0: in LOAD(st) after its fragment
-// reads; 1: in MFMA(st), one after every 8 MFMAs; 2: the two A ops in LOAD(st), the two B ops in
-// MFMA(st).  (An LDS-DMA op costs its wave ~60 issue cycles among bare MFMAs but 100-185 inside a
-// phase that also reads fragments: MI355X_MICROARCH cycle constants.)
-// SKEL (timing skeletons, never shipped, LLMT_WPP_SKEL): 1 = no fills inside the loop (every stage
-// re-reads the prologue's data); with LLMT_WPP_FILL=1 also 2 = global loads only (never written to
-// LDS), 3 = LDS writes of stale registers only (no loads) — to price each part of the fill.
-// FILL: 0 = LDS-DMA fills (PLACE / NSL as above); 1 = register-staged fills: each wave loads its
-// 4 x 16 bytes of stage st+3 into VGPRs (two register sets, stage parity) in LOAD(st) and writes
-// stage st+1's (loaded two phases earlier) to LDS with 16-byte lane-linear ds_write_b128 — the same
-// LDS image as the DMA fill.  Measured without fills the schedule runs 1.4-1.5 PF (LLMT_WPP_SKEL=1):
-// the LDS-DMA issue inside LOAD was what kept it at ~1.1.  With register staging a slot is free one
-// phase after its last read, so NSL = 2 (64 KiB) is legal as well as 4.
-template <int MODE, int PLACE, int NSL, int SKEL = 0, int FILL = 0>
+// Fills are register-staged: in LOAD(st) each wave writes stage st+1 (loaded two phases earlier)
+// into its ring slot with 16-byte lane-linear ds_write_b128 and loads stage st+3 into the freed
+// registers (two register sets, stage parity).  A slot is free one phase after its last read, so two
+// 32 KiB slots suffice, and half the LDS is left for other kernels' workgroups on the CU.  (Measured
+// against LDS-DMA fills through a 4-slot ring: +2-4 % op level, +0.5 % in the step; the LDS-DMA op
+// costs its wave ~60-185 issue cycles inside a phase that also reads fragments, docs/round4.md.)
+template <int MODE>
 __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
     const bf16_raw* __restrict__ A, int lda, const bf16_raw* __restrict__ B, int ldb, float* __restrict__ C,
     int ldc, int M, int N, int K, int tiles, int tiles_k, int m_chunk, int split, int nwg, float* __restrict__ slab,
     float* __restrict__ bias_slab) {
-  constexpr int NS = NSL, D = NSL - 1;  // ring slots; stage st+D is filled while stage st is read
+  constexpr int NS = 2;  // ring slots
   __shared__ __attribute__((aligned(16))) bf16_raw smem[NS * SLOT / 2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -140,9 +114,8 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
   const int nst = (rows + BR - 1) / BR;
   const bool want_bias = bias_slab != nullptr && tile_k == 0;
 
-
-  // fill ops: this wave copies image rows 4*wave .. 4*wave+3 of A and of B (two 1-KiB ops each);
-  // lane l lands at LDS chunk (l & 31) of row 2*op + (l >> 5) and holds the source chunk whose
+  // fills: this wave copies image rows 4*wave .. 4*wave+3 of A and of B (two 1-KiB pieces each);
+  // lane l lands at LDS chunk (l & 31) of row 2*j + (l >> 5) and holds the source chunk whose
   // 32-byte segment is that one XOR f(row)
   int voa[2], vob[2];
 #pragma unroll
@@ -154,35 +127,6 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
     vob[j] = (row * ldb + k0 + 8 * csrc) * 2;
   }
   const unsigned lds = (unsigned)(unsigned long)(lds_void*)smem;
-  // one buffer descriptor per stage (base = the stage's first row, records = its rows): rows past
-  // the chunk read as zero, and no 32-bit offset ever spans more than one stage (the LM head's
-  // 50304-wide rows need no minimum split)
-  // fill op j (0, 1: A rows; 2, 3: B rows) of stage st into ring slot `slot`
-  auto fill_op = [&](int st, int slot, int j) {
-    const unsigned base = lds + slot * SLOT + wave * 2048;
-    const int r0 = st * BR, nr = min(BR, rows - r0);
-    if (j < 2) {
-      const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(A + (long)(m_begin + r0) * lda), (short)0, nr * lda * 2, 0x00020000);
-      dma16(base + j * 1024, voa[j], ra, 0);
-    } else {
-      const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(B + (long)(m_begin + r0) * ldb), (short)0, nr * ldb * 2, 0x00020000);
-      dma16(base + IMG + (j - 2) * 1024, vob[j - 2], rb, 0);
-    }
-  };
-  auto fill = [&](int st, int slot) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fill_op(st, slot, j);
-  };
-  // fill ops issued after stage st+1's last one at the wait in LOAD(st) (see PLACE)
-  auto younger = [&](int st) {
-    int n = 0;
-#pragma unroll
-    for (int s = 2; s < D; ++s) n += st + s < nst ? 4 : 0;  // whole stages issued in earlier phases
-    if (st + D < nst) n += PLACE == 0 ? 4 : PLACE == 2 ? 2 : 0;  // this LOAD's own ops
-    return n;
-  };
 
   // fragment read addresses (bytes within a slot): lane (g, q, p) reads rows 8g + q (+4) at the
   // 32-byte segment (logical ^ f), bytes 8p..8p+7; A fragments are taken in an order rotated by
@@ -206,7 +150,7 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
 
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
-  u32x4 R0[4], R1[4], R2[4];  // register-staged fills: FILL 1 stage parity (R0, R1); FILL 2 stage % 3
+  u32x4 R0[4], R1[4];  // staged stage parity
   // (unconditional: a stage past the chunk has a zero-record descriptor and loads zeros — a
   // conditional load made hipcc drain every outstanding load before each LDS write)
   auto load_stage = [&](int st, u32x4 (&R)[4]) {
@@ -226,214 +170,50 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
     *(lds_u32x4*)(size_t)(a + IMG + 1024) = R[3];
   };
 
-  // prologue: stage 0 landed everywhere (DMA: stages 1..D-1 in flight; registers: stages 1 and 2
-  // loading); Y then falls one barrier behind
-  if (FILL == 0) {
-#pragma unroll
-    for (int s = 0; s < NS - 1; ++s)
-      if (s < nst) fill(s, s);
-    wait_fill_barrier(4 * min(nst - 1, D - 1));
-  } else if (FILL == 3) {
-    // X keeps stage s in set s & 1, Y in set (s + 1) & 1, so both use set (st + 1) & 1 in phase st:
-    // X writes stages 0 (and 1, rewritten in MFMA(0)), Y stages 0 and 1; then X loads 1, 2 and
-    // Y loads 2, 3 (older load first: the set written next is the one that must have landed)
-    load_stage(wn, R0);
-    load_stage(1 - wn, R1);
-    write_stage(wn, R0);
-    write_stage(1 - wn, R1);
-    load_stage(1 + wn, R1);
-    load_stage(2 + wn, R0);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  } else {
-    load_stage(0, R0);
-    load_stage(1, R1);
-    if (FILL == 2) load_stage(2, R2);
-    write_stage(0, R0);
-    load_stage(FILL == 2 ? 3 : 2, R0);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  }
+  // prologue: stage 0 landed everywhere, stages 1 and 2 loading; Y then falls one barrier behind
+  load_stage(0, R0);
+  load_stage(1, R1);
+  write_stage(0, R0);
+  load_stage(2, R0);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   if (wn == 1) barrier();
 
-  unsigned long long pr[6] = {0, 0, 0, 0, 0, 0}, pt2 = 0, pt3 = 0, pt4 = 0, pt5 = 0;
   // R: the register set of stage st+1 (= that of st+3)
   auto phase = [&](int st, int slot, u32x4 (&R)[4]) {
-    // ---- LOAD(st): fragments of stage st, fill of stage st+3 into the slot of stage st-1
+    // ---- LOAD(st): fragments of stage st, stage st+1 into the other slot, stage st+3 loading
     const unsigned sb = lds + slot * SLOT;
-    unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
-    if (SKEL == 9) {
-      __builtin_amdgcn_sched_barrier(0);
-      t0 = __builtin_amdgcn_s_memtime();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    const bool refill = FILL == 0 && SKEL == 0 && st + D < nst;
-    const int fslot = slot == 0 ? NS - 1 : slot - 1;  // the slot of stage st-1 = that of st+D
     bf16x8 af[FA], bfr[FB];
 #pragma unroll
     for (int i = 0; i < FA; ++i) af[i] = tr_read(sb + ao[i]);
 #pragma unroll
     for (int j = 0; j < FB; ++j) bfr[j] = tr_read(sb + bo[j]);
-    if (SKEL == 9) {
-      __builtin_amdgcn_sched_barrier(0);
-      t1 = __builtin_amdgcn_s_memtime();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (refill) {
-      if (PLACE == 0) fill(st + D, fslot);
-      if (PLACE == 2) {
-        fill_op(st + D, fslot, 0);
-        fill_op(st + D, fslot, 1);
-      }
-    }
-    if (FILL == 0) {
-      wait_fill_barrier(younger(st));
-    } else if (FILL == 3) {
-      if (SKEL == 9) t2 = t1;
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    } else {
-      // stage st+1 (loaded two phases ago) into its slot, stage st+3 into the freed registers; both
-      // unconditional (a slot past the last stage is never read)
-      if (SKEL == 0 || SKEL == 3 || SKEL == 9) write_stage(slot + 1 == NS ? 0 : slot + 1, R);  // 3: stale data
-      if (SKEL == 0 || SKEL == 2 || SKEL == 9) load_stage(st + (FILL == 2 ? 4 : 3), R);
-      if (SKEL == 9) {
-        __builtin_amdgcn_sched_barrier(0);
-        t2 = __builtin_amdgcn_s_memtime();
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (SKEL == 2) {  // loads kept live, never written to LDS
-#pragma unroll
-        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(R[j]));
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
+    // both unconditional (a slot past the last stage is never read)
+    write_stage(slot ^ 1, R);
+    load_stage(st + 3, R);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     // ---- MFMA(st)
     __builtin_amdgcn_sched_barrier(0);
-    if (SKEL == 9) {
-      // every stamp issued so far has returned (lgkmcnt(0) above): account them here, where the
-      // compiler's own wait costs nothing; this phase's t3..t5 are accounted one phase later
-      pr[0] += t1 - t0;  // fragment reads issued
-      pr[1] += t2 - t1;  // LDS writes + global loads issued
-      if (pt2 != 0) {
-        pr[2] += pt3 - pt2;  // wait for own LDS ops + barrier A (+ first MFMA)
-        pr[3] += pt4 - pt3;  // remaining MFMA issue
-        pr[4] += pt5 - pt4;  // barrier B
-        pr[5] += 1;
-      }
-      pt2 = t2;
-      __builtin_amdgcn_sched_barrier(0);
-    }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < FA; ++i) {
+    for (int i = 0; i < FA; ++i)
 #pragma unroll
-      for (int j = 0; j < FB; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-        if (SKEL == 9 && i == 0 && j == 0) {  // after the compiler's fragment wait
-          __builtin_amdgcn_sched_barrier(0);
-          t3 = __builtin_amdgcn_s_memtime();
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      // fill ops between MFMA groups (the slot of stage st-1 is free: every wave finished reading
-      // it before the barrier that opened this segment)
-      if (FILL == 0 && ((PLACE == 1 && (i & 1)) || (PLACE == 2 && (i == 3 || i == 7)))) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (refill) fill_op(st + D, fslot, PLACE == 1 ? i >> 1 : (i == 3 ? 2 : 3));
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      // FILL 3: the fill rides in this wave's own MFMA segment.  X writes stage st+1 into the slot
-      // of stage st-1 (Y's last reads of it ended a barrier before this segment opened) and loads
-      // stage st+3; Y, one barrier later, writes stage st+2 into the slot of stage st (every wave
-      // finished reading it at the barrier that opened this segment) and loads stage st+4; each
-      // group's writes land before the barrier closing the segment, ahead of the first reader.
-      // Parts: A-row writes, B-row writes, A loads, B loads.
-      const int part = PLACE == 1 ? ((i & 1) ? i >> 1 : -1) : (i < 4 ? i : -1);
-      if (FILL == 3 && part >= 0) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (part < 2) {
-          const unsigned a = lds + ((st + 1 - wn) & 1) * SLOT + wave * 2048 + 16 * lane + part * IMG;
-          *(lds_u32x4*)(size_t)a = R[2 * part];
-          *(lds_u32x4*)(size_t)(a + 1024) = R[2 * part + 1];
-        } else {
-          const int ls = st + 3 + wn, r0 = ls * BR, nr = max(0, min(BR, rows - r0));
-          if (part == 2) {
-            const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(A + (long)(m_begin + r0) * lda, nr * lda * 2);
-            R[0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, voa[0], 0, 0));
-            R[1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, voa[1], 0, 0));
-          } else {
-            const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(B + (long)(m_begin + r0) * ldb, nr * ldb * 2);
-            R[2] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, vob[0], 0, 0));
-            R[3] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, vob[1], 0, 0));
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
+      for (int j = 0; j < FB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     if (want_bias) {
       bacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], ones, bacc[0], 0, 0, 0);
       bacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], ones, bacc[1], 0, 0, 0);
     }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
-    if (SKEL == 9) {
-      t4 = __builtin_amdgcn_s_memtime();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (FILL == 3) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // own writes landed
-    else barrier();
-    if (SKEL == 9) {
-      __builtin_amdgcn_sched_barrier(0);
-      pt5 = __builtin_amdgcn_s_memtime();
-      __builtin_amdgcn_sched_barrier(0);
-      pt3 = t3;
-      pt4 = t4;
-    }
+    barrier();
   };
-  if (NS == 5) {
-    for (int s0 = 0; s0 < nst; s0 += 5) {  // (DMA only; registers unused)
-      phase(s0, 0, R1);
-      if (s0 + 1 < nst) phase(s0 + 1, 1, R0);
-      if (s0 + 2 < nst) phase(s0 + 2, 2, R1);
-      if (s0 + 3 < nst) phase(s0 + 3, 3, R0);
-      if (s0 + 4 < nst) phase(s0 + 4, 4, R1);
-    }
-  } else if (FILL == 2) {
-    // three register sets: a stage's loads get three phases (not two) to land before its LDS write;
-    // groups of 6 unconditional phases (2 slots x 3 sets), zero stages past the chunk
-    for (int s0 = 0; s0 < nst; s0 += 6) {
-      phase(s0, 0, R1);
-      phase(s0 + 1, 1, R2);
-      phase(s0 + 2, 0, R0);
-      phase(s0 + 3, 1, R1);
-      phase(s0 + 4, 0, R2);
-      phase(s0 + 5, 1, R0);
-    }
-  } else if ((FILL == 1 || FILL == 3) && NS == 2) {
-    // register-staged, 2 slots: pairs of phases with no per-phase condition (a conditional phase
-    // made hipcc assume the loads of a skipped phase were never issued and drain vmcnt early); an
-    // odd last stage is padded with a stage of zeros (zero-record loads, MFMAs on zeros)
-    for (int s0 = 0; s0 < nst; s0 += 2) {
-      phase(s0, 0, R1);
-      phase(s0 + 1, 1, R0);
-    }
-  } else {
-    for (int s0 = 0; s0 < nst; s0 += 4) {  // stage parity and slot are compile-time in each step
-      phase(s0, 0, R1);
-      if (s0 + 1 < nst) phase(s0 + 1, 1 % NS, R0);
-      if (s0 + 2 < nst) phase(s0 + 2, 2 % NS, R1);
-      if (s0 + 3 < nst) phase(s0 + 3, 3 % NS, R0);
-    }
+  // pairs of phases with no per-phase condition (a conditional phase made hipcc assume the loads
+  // of a skipped phase were never issued and drain vmcnt early); an odd last stage is padded with a
+  // stage of zeros (zero-record loads, MFMAs on zeros)
+  for (int s0 = 0; s0 < nst; s0 += 2) {
+    phase(s0, 0, R1);
+    phase(s0 + 1, 1, R0);
   }
   if (wn == 0) barrier();  // X matches Y's extra barrier
-  if (SKEL == 9) {  // the last phase
-    pr[2] += pt3 - pt2;
-    pr[3] += pt4 - pt3;
-    pr[4] += pt5 - pt4;
-    pr[5] += 1;
-  }
-  if (SKEL == 9 && g_wpp_probe != nullptr && blockIdx.x < 256 && lane == 0) {
-#pragma unroll
-    for (int e = 0; e < 6; ++e) g_wpp_probe[(blockIdx.x * 8 + wave) * 8 + e] = pr[e];
-  }
 
   // ---- epilogue.  Accumulator (i, j) register r of lane l: n = n0 + 128 wn + 16 ((i + 2wk) & 7)
   // + 4 (l >> 4) + r, k = k0 + 64 wk + 16 j + (l & 15)
@@ -568,13 +348,6 @@ PPPlan plan_pp(int M, int N, int K, int split_req, int mode_req, int ncu, int mi
 }
 
 hipError_t plan_wgrad_pp(int lda, int ldb, int M, int N, int K, int split, int mode, bool det, PPPlan& p) {
-  // LLMT_WPP_EPI=atomic|slab: the auto plan's split-K epilogue in fast mode (A/B knob)
-  static const int epi = [] {
-    const char* e = std::getenv("LLMT_WPP_EPI");
-    if (e == nullptr) return -1;
-    return std::string(e) == "atomic" ? 2 : std::string(e) == "slab" ? 0 : -1;
-  }();
-  if (mode < 0) mode = epi;
   if (lda % 8 || ldb % 8 || K % 8 || lda < N) return hipErrorInvalidValue;
   // one stage of either operand must stay below the 32-bit buffer range
   if ((long long)wpp::BR * std::max(lda, ldb) * 2 >= (1LL << 31)) return hipErrorInvalidValue;
@@ -583,11 +356,6 @@ hipError_t plan_wgrad_pp(int lda, int ldb, int M, int N, int K, int split, int m
   return hipSuccess;
 }
 }  // namespace
-
-hipError_t wgrad_pp_set_probe(void* buf) {
-  unsigned long long* p = (unsigned long long*)buf;
-  return hipMemcpyToSymbol(HIP_SYMBOL(wpp::g_wpp_probe), &p, sizeof(p));
-}
 
 long wgrad_pp_ws_floats(int lda, int ldb, int M, int N, int K, int split, int mode, bool bias) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
@@ -612,96 +380,18 @@ hipError_t launch_wgrad_pp(const void* dy, int lda, const void* x, int ldb, floa
       bias == nullptr ? nullptr : atomic ? bias : ws + (slabs ? (long)p.tiles * p.split * wpp::SLAB_FLOATS : 0);
   if ((slabs || (bias != nullptr && !atomic)) && ws == nullptr) return hipErrorInvalidValue;
   const int m = slabs ? 0 : (p.split == 1 ? 1 : 2);
-  // A/B knobs of the schedule (docs/round4.md): LLMT_WPP_PLACE (fill-op placement, 0 / 2),
-  // LLMT_WPP_SLOTS (4 or 5 ring slots = 128 / 160 KiB of LDS)
-  static const int place = [] {
-    const char* e = std::getenv("LLMT_WPP_PLACE");
-    return e != nullptr ? std::atoi(e) : 0;
-  }();
-  static const int skel = [] {
-    const char* e = std::getenv("LLMT_WPP_SKEL");
-    return e != nullptr ? std::atoi(e) : 0;
-  }();
-  // default: register-staged fills through a 2-slot (64 KiB) ring (op level +2-4 % over LDS-DMA
-  // on one box, a tie on another; step +0.5 % at mb 128: profiles/r4/wgrad/ab_fill_mb*.txt) —
-  // half the LDS leaves room for main-stream workgroups on the same CU
-  static const int fillmode = [] {
-    const char* e = std::getenv("LLMT_WPP_FILL");
-    return e != nullptr ? std::atoi(e) : 1;
-  }();
-  static const int slots = [] {
-    const char* e = std::getenv("LLMT_WPP_SLOTS");
-    const int v = e != nullptr ? std::atoi(e) : (fillmode == 1 || fillmode == 3 ? 2 : 4);
-    return v == 5 || v == 2 ? v : 4;
-  }();
-#define LLMT_PP_LAUNCH(MD, PL, NSL)                                                                             \
-  hipLaunchKernelGGL((wpp::wgrad_pp_kernel<MD, PL, NSL>), dim3(nwg), dim3(wpp::kThreads), 0, stream,             \
-                     (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k,     \
-                     p.m_chunk, p.split, nwg, slab, bias_parts)
-#define LLMT_PP_MODES(PL, NSL)                \
-  if (m == 0) LLMT_PP_LAUNCH(0, PL, NSL);      \
-  else if (m == 1) LLMT_PP_LAUNCH(1, PL, NSL); \
-  else LLMT_PP_LAUNCH(2, PL, NSL);
-#define LLMT_RS_LAUNCH(MD, NSL, SK)                                                                       \
-  hipLaunchKernelGGL((wpp::wgrad_pp_kernel<MD, 0, NSL, SK, 1>), dim3(nwg), dim3(wpp::kThreads), 0, stream,  \
-                     (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k, \
-                     p.m_chunk, p.split, nwg, slab, bias_parts)
-  if (fillmode == 2) {
-    if (m == 0) hipLaunchKernelGGL((wpp::wgrad_pp_kernel<0, 0, 2, 0, 2>), dim3(nwg), dim3(wpp::kThreads), 0, stream,
-                                   (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles,
-                                   p.tiles_k, p.m_chunk, p.split, nwg, slab, bias_parts);
-    else if (m == 1) hipLaunchKernelGGL((wpp::wgrad_pp_kernel<1, 0, 2, 0, 2>), dim3(nwg), dim3(wpp::kThreads), 0,
-                                        stream, (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K,
-                                        p.tiles, p.tiles_k, p.m_chunk, p.split, nwg, slab, bias_parts);
-    else hipLaunchKernelGGL((wpp::wgrad_pp_kernel<2, 0, 2, 0, 2>), dim3(nwg), dim3(wpp::kThreads), 0, stream,
-                            (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k,
-                            p.m_chunk, p.split, nwg, slab, bias_parts);
-  } else if (fillmode == 3) {
-#define LLMT_RS3_LAUNCH(MD, PL, SK)                                                                        \
-  hipLaunchKernelGGL((wpp::wgrad_pp_kernel<MD, PL, 2, SK, 3>), dim3(nwg), dim3(wpp::kThreads), 0, stream,    \
-                     (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k, \
-                     p.m_chunk, p.split, nwg, slab, bias_parts)
-    if (skel == 9 && m == 0) {
-      if (place == 1) LLMT_RS3_LAUNCH(0, 1, 9);
-      else LLMT_RS3_LAUNCH(0, 0, 9);
-    } else if (place == 1) {
-      if (m == 0) LLMT_RS3_LAUNCH(0, 1, 0);
-      else if (m == 1) LLMT_RS3_LAUNCH(1, 1, 0);
-      else LLMT_RS3_LAUNCH(2, 1, 0);
-    } else {
-      if (m == 0) LLMT_RS3_LAUNCH(0, 0, 0);
-      else if (m == 1) LLMT_RS3_LAUNCH(1, 0, 0);
-      else LLMT_RS3_LAUNCH(2, 0, 0);
-    }
-#undef LLMT_RS3_LAUNCH
-  } else if (fillmode == 1) {
-    if (skel == 1) LLMT_RS_LAUNCH(0, 4, 1);
-    else if (skel == 9 && m == 0) LLMT_RS_LAUNCH(0, 2, 9);  // slab epilogue only
-    else if (skel == 2) LLMT_RS_LAUNCH(0, 2, 2);
-    else if (skel == 3) LLMT_RS_LAUNCH(0, 2, 3);
-    else if (slots == 2) {
-      if (m == 0) LLMT_RS_LAUNCH(0, 2, 0);
-      else if (m == 1) LLMT_RS_LAUNCH(1, 2, 0);
-      else LLMT_RS_LAUNCH(2, 2, 0);
-    } else {
-      if (m == 0) LLMT_RS_LAUNCH(0, 4, 0);
-      else if (m == 1) LLMT_RS_LAUNCH(1, 4, 0);
-      else LLMT_RS_LAUNCH(2, 4, 0);
-    }
-  } else if (skel == 1) {
-    hipLaunchKernelGGL((wpp::wgrad_pp_kernel<0, 0, 4, 1>), dim3(nwg), dim3(wpp::kThreads), 0, stream,
-                       (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k,
-                       p.m_chunk, p.split, nwg, slab, bias_parts);
-  } else if (slots == 5) {
-    if (place == 2) { LLMT_PP_MODES(2, 5) }
-    else { LLMT_PP_MODES(0, 5) }
-  } else {
-    if (place == 2) { LLMT_PP_MODES(2, 4) }
-    else { LLMT_PP_MODES(0, 4) }
-  }
-#undef LLMT_PP_MODES
-#undef LLMT_PP_LAUNCH
-#undef LLMT_RS_LAUNCH
+  if (m == 0)
+    hipLaunchKernelGGL(wpp::wgrad_pp_kernel<0>, dim3(nwg), dim3(wpp::kThreads), 0, stream, (const bf16_raw*)dy, lda,
+                       (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k, p.m_chunk, p.split, nwg, slab,
+                       bias_parts);
+  else if (m == 1)
+    hipLaunchKernelGGL(wpp::wgrad_pp_kernel<1>, dim3(nwg), dim3(wpp::kThreads), 0, stream, (const bf16_raw*)dy, lda,
+                       (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k, p.m_chunk, p.split, nwg, slab,
+                       bias_parts);
+  else
+    hipLaunchKernelGGL(wpp::wgrad_pp_kernel<2>, dim3(nwg), dim3(wpp::kThreads), 0, stream, (const bf16_raw*)dy, lda,
+                       (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k, p.m_chunk, p.split, nwg, slab,
+                       bias_parts);
   const long total = slabs ? (long)p.tiles * 8 * wpp::NACC * 64 : 0;
   const int nbias = bias != nullptr && !atomic ? N : 0;
   if (total + nbias > 0)

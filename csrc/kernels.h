@@ -142,27 +142,12 @@ constexpr int kSumsqBlocks = 1024;
 hipError_t launch_sumsq(const float* x, long long n, float* partials, float* out,
                         hipStream_t stream);
 
-// ---- weight-gradient GEMM: C[N, K] (f32) += dY[M, N]^T X[M, K] (bf16), split-K + atomics --
-// split <= 0 / tile == 0 let the launcher's cost model choose (tile 128 or 256 forces one).
-// Deterministic mode: `det_ws` (wgrad_gemm_det_ws_floats(...) floats) receives per-chunk partial
-// slabs that are reduced into C in a fixed order instead of the split-K atomics.
-long wgrad_gemm_det_ws_floats(int lda, int ldb, int M, int N, int K, int split, int tile);
-
 // Ping-pong weight-gradient GEMM (gemm_wgrad_pp.hip): C[N,K] += dy^T x and, with `bias`,
 // bias[N] += colsum(dy).  `ws` holds wgrad_pp_ws_floats(...) floats (split slabs + bias parts).
 // mode: -1 auto, 0 slabs + fixed-order reduce, 2 fp32 atomics (ignored in deterministic mode).
-// Timing probe buffer of the SKEL 9 kernel (LLMT_WPP_SKEL=9; nullptr disables)
-hipError_t wgrad_pp_set_probe(void* buf);
 long wgrad_pp_ws_floats(int lda, int ldb, int M, int N, int K, int split, int mode, bool bias);
 hipError_t launch_wgrad_pp(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N, int K,
                            int split, int mode, float* ws, float* bias, hipStream_t stream);
-// `pipe`: 0 = the plain 256-tile kernel (332 registers per lane: other kernels' waves can share
-// its SIMDs — the side-stream default), 4 / 5 = the software-pipelined one with that many ring
-// slots (all 512 registers: nothing else runs beside it — for GEMMs that own the chip), -1 = the
-// default (0).
-hipError_t launch_wgrad_gemm(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N,
-                             int K, int split, int tile, hipStream_t stream, float* det_ws = nullptr, int pipe = -1);
-
 // ---- forward / data-gradient GEMM with fused epilogues (bf16 in, fp32 accumulate, bf16 out)
 // C[M, N] = epi(A[M, K] . op(B)); B is [N, ldb] (K contiguous, b_kn = false) or [K, ldb]
 // (N contiguous, b_kn = true).  epilogue 0: C = acc + bias (bias optional);
@@ -189,13 +174,6 @@ struct GemmFusedArgs {
 };
 hipError_t launch_gemm_fused(const GemmFusedArgs& args, hipStream_t stream);
 
-// Ping-pong GEMM (gemm_pp.hip): c[M,N] = bf16(x[M,K] w[N,K]^T + bias) (kn = false; epi 1 also
-// c2 = bf16(gelu(c))) or c = bf16(x[M,K] w[K,N]) (kn = true, data gradient; epi 2: c = bf16(acc *
-// gelu'(c2)), c2 = the pre-activation u; epi 3: delta[b, h, t] = sum over head h's 64 columns of
-// c * c2 (c2 = the attention output O), T = sequence length).  Needs K % 64 == 0, N % 8 == 0.
-bool gemm_pp_supported(int M, int N, int K, int ldx, int ldw, int ldc, bool kn);
-hipError_t launch_gemm_pp(const void* x, int ldx, const void* w, int ldw, const void* bias, void* c, void* c2, int ldc,
-                          int M, int N, int K, int epi, bool kn, float* delta, int T, hipStream_t stream);
 inline long gemm_fused_ws_floats(int M, int N) {
   const int nparts = (M + 127) / 128;
   return (long)nparts * N + colsum_scratch_floats(nparts, N);

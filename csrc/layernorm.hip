@@ -11,7 +11,6 @@
 // register partials over a grid-stride run of rows, a cross-wave LDS reduction, then one fp32
 // atomic per column per workgroup.
 #include <algorithm>
-#include <cstdlib>
 
 #include "common.h"
 #include "kernels.h"

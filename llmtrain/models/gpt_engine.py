@@ -236,7 +236,7 @@ class FusedGPTEngine:
                 ops.wgrad_accum(dst, dy, x, bias=bias)
             self._pending.extend((dy, x))
         else:  # one stream: nothing runs beside it
-            ops.wgrad_accum(dst, dy, x, bias=bias, exclusive=True)
+            ops.wgrad_accum(dst, dy, x, bias=bias)
 
     def _retire_block(self) -> None:
         """End of one block's backward: fence its side-stream GEMMs with an event and release the
@@ -400,7 +400,7 @@ class FusedGPTEngine:
         if dlogits.is_cuda and dlogits.dtype == torch.bfloat16:
             # split-K MFMA kernel: 9.78 vs 10.34 ms for hipBLASLt's fp32-output GEMM at 128K tokens
             # (bench/head_wgrad.py; N = 50257 rows inside the 50304-wide padded logits)
-            ops.wgrad_accum(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled, exclusive=True)
+            ops.wgrad_accum(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled)
         else:
             accumulate_wgrad(self._g(self.head_weight), dlogits[:, : self.vocab], hf_scaled)
         del hf_scaled

@@ -8,7 +8,9 @@ op and no silent fallback: a GPU tensor with the extension missing raises (``_ex
 
 from __future__ import annotations
 
+import contextlib
 import os
+from collections.abc import Iterator
 
 import torch
 
@@ -30,18 +32,20 @@ __all__ = [
     "head_dx",
     "head_logits",
     "hip_ops",
+    "kernel_policy",
     "layernorm_bwd",
     "linear_dx",
     "linear_dx_gelu_bwd",
     "linear_fwd",
     "linear_fwd_gelu",
     "ln_param_reduce",
+    "policy_state",
+    "restore_policy",
     "scale",
     "set_deterministic",
     "single_stream",
     "sumsq",
     "wgrad_accum",
-    "wgrad_fuses_bias",
 ]
 
 
@@ -58,9 +62,11 @@ _POLICY = {"gemm_all_ours": False, "single_stream": False, "deterministic": Fals
 
 # How run.deterministic keeps the step bitwise reproducible (LLMTRAIN_DET_SCHEDULE overrides):
 #  * "serial": the weight-gradient GEMMs run on the main stream (no side stream), the forward / dX
-#    GEMMs stay on hipBLASLt's tuned solutions.  Nothing runs beside a library GEMM, so the timing
-#    perturbation that made hipBLASLt's Stream-K solutions diverge (docs/round3.md section 2) is
-#    gone; costs the overlap of the two streams (~1 %).
+#    GEMMs stay on hipBLASLt's tuned solutions except the LM-head dX (our kernel: the one library
+#    GEMM measured non-reproducible in this schedule, docs/round4.md section 3).  Evidence for the
+#    library GEMMs that remain: bitwise-equal repeats at micro-batch 8 and 32 of GPT-2 124M
+#    (bench/determinism_probe.py, profiles/r4/det/); other shapes are unpinned, and every library
+#    GEMM of a deterministic run is named once by a warning (_det_fallback).
 #  * "ours": every forward / dX GEMM on the hand-written kernel (csrc/gemm_fused.hip), side stream
 #    kept; slower because that kernel trails hipBLASLt at 128K rows (docs/round4.md).
 DET_SCHEDULES = ("serial", "ours")
@@ -73,10 +79,12 @@ def set_deterministic(on: bool, schedule: str | None = None) -> bool:
     becomes one of :data:`DET_SCHEDULES` — hipBLASLt's Stream-K solutions combine partial tiles in
     an order that depends on which workgroups finish first, which the weight-gradient side stream
     perturbs (bench/determinism_probe.py --runs, docs/round3.md).  Returns the previous setting.
-    The CPU reference ops are deterministic anyway."""
-    schedule = schedule or os.environ.get("LLMTRAIN_DET_SCHEDULE", "serial")
-    if schedule not in DET_SCHEDULES:
-        raise ValueError(f"deterministic schedule must be one of {DET_SCHEDULES}, not {schedule!r}")
+    The CPU reference ops are deterministic anyway.  Prefer :func:`kernel_policy`, which restores
+    the previous policy on exit (the Trainer scopes its steps with it)."""
+    if on:
+        schedule = schedule or os.environ.get("LLMTRAIN_DET_SCHEDULE", "serial")
+        if schedule not in DET_SCHEDULES:
+            raise ValueError(f"deterministic schedule must be one of {DET_SCHEDULES}, not {schedule!r}")
     _POLICY["gemm_all_ours"] = bool(on) and schedule == "ours"
     _POLICY["single_stream"] = bool(on) and schedule == "serial"
     _POLICY["deterministic"] = bool(on)
@@ -85,6 +93,34 @@ def set_deterministic(on: bool, schedule: str | None = None) -> bool:
     prev = bool(torch.ops.llmtrain_hip.get_deterministic())
     torch.ops.llmtrain_hip.set_deterministic(bool(on))
     return prev
+
+
+def policy_state() -> tuple[dict[str, bool], bool]:
+    """Snapshot of the process-wide kernel policy: the Python routing flags and the C++
+    deterministic flag (False when the extension is not loaded)."""
+    cpp = bool(torch.ops.llmtrain_hip.get_deterministic()) if _ext.is_loaded() else False
+    return dict(_POLICY), cpp
+
+
+def restore_policy(state: tuple[dict[str, bool], bool]) -> None:
+    """Undo every policy change since :func:`policy_state` returned ``state``."""
+    flags, cpp = state
+    _POLICY.update(flags)
+    if _ext.is_loaded():
+        torch.ops.llmtrain_hip.set_deterministic(bool(cpp))
+
+
+@contextlib.contextmanager
+def kernel_policy(deterministic: bool, schedule: str | None = None) -> Iterator[None]:
+    """Run a block under ``run.deterministic = deterministic`` and restore the previous policy on
+    exit, so one Trainer's setting never leaks into the next one in the same process (a test
+    suite, a notebook)."""
+    prev = policy_state()
+    set_deterministic(deterministic, schedule)
+    try:
+        yield
+    finally:
+        restore_policy(prev)
 
 
 def single_stream() -> bool:
@@ -277,17 +313,43 @@ _WARNED: set[str] = set()
 
 
 def _det_fallback(what: str, always: bool = False) -> None:
-    """Deterministic mode promises every forward / dX GEMM on the hand-written kernel; a shape it
-    cannot take runs on hipBLASLt, whose Stream-K solutions are not run-to-run reproducible beside
-    the weight-gradient side stream.  Say so once per distinct case instead of failing silently."""
+    """A GEMM of a deterministic run that cannot take the hand-written fixed-order kernel (its
+    shape or alignment is outside what csrc/gemm_fused.hip takes: K % 64 == 0, K >= 256, N % 8 ==
+    0, 16-byte aligned operands) runs on hipBLASLt instead, whose split / Stream-K solutions may
+    combine partial sums in completion order.  In the "ours" schedule (every GEMM promised on our
+    kernel), and for the GEMMs the serial schedule keeps off the library (``always``), that breaks
+    the promise: say so once per distinct case instead of failing silently."""
     if (_POLICY["gemm_all_ours"] or (always and _POLICY["deterministic"])) and what not in _WARNED:
         _WARNED.add(what)
         import warnings
 
         warnings.warn(
-            f"run.deterministic: {what} runs on hipBLASLt (not bitwise reproducible run to run); "
-            "set LLMTRAIN_WGRAD_STREAM=0 for a reproducible schedule", RuntimeWarning, stacklevel=3,
+            f"run.deterministic: {what} cannot take the fixed-order GEMM kernel and runs on hipBLASLt "
+            "(bitwise run-to-run reproducibility of this GEMM is not guaranteed)", RuntimeWarning, stacklevel=3,
         )
+
+
+def _det_library(what: str) -> None:
+    """Serial deterministic schedule: ``what`` runs on a tuned hipBLASLt solution by design.  Those
+    were bitwise reproducible in every repeat measured (GPT-2 124M at micro-batch 8 and 32,
+    profiles/r4/det/), which pins no other shape: name each such GEMM once in the log, so a run on a
+    new shape knows which of its GEMMs rest on that evidence (LLMTRAIN_DET_SCHEDULE=ours moves every
+    one the kernel can take onto the fixed-order kernel)."""
+    if _POLICY["single_stream"] and what not in _WARNED:
+        _WARNED.add(what)
+        import logging
+
+        logging.getLogger(__name__).warning(
+            "run.deterministic (serial schedule): %s runs on hipBLASLt; its reproducibility is measured "
+            "for GPT-2 124M at micro-batch 8/32 only", what,
+        )
+
+
+def _lib_mm(a: torch.Tensor, b_t: torch.Tensor, bias: torch.Tensor | None = None, *, op: str) -> torch.Tensor:
+    """``a @ b_t (+ bias)`` on the library GEMM, logged once per shape in the serial schedule."""
+    if _POLICY["single_stream"] and a.is_cuda:
+        _det_library(f"GEMM {op} M={a.shape[0]} K={a.shape[1]} N={b_t.shape[1]}")
+    return torch.mm(a, b_t) if bias is None else torch.addmm(bias, a, b_t)
 
 
 def _fgemm_ok(a: torch.Tensor, k: int, n: int, *others: torch.Tensor | None, op: str = "") -> bool:
@@ -333,24 +395,6 @@ def _gemm_rows(a, b, b_kn: bool, epilogue: int, bias=None, u=None, dbias=None, s
     return out, torch.cat([p[1] for p in parts])
 
 
-# GEMMs on the ping-pong kernel (csrc/gemm_pp.hip), by call site: LLMTRAIN_GEMM_PP = comma list of
-# fwd (linear_fwd), fwd_gelu, dx (linear_dx), dx_gelu (linear_dx_gelu_bwd), dx_attn
-# (linear_dx_attn); "all" = every one.  One
-# 256x256 tile per workgroup, no split-K: deterministic in both modes.
-_GPP_SITES = {"fwd", "fwd_gelu", "dx", "dx_gelu", "dx_attn"}
-GEMM_PP = frozenset(_GPP_SITES if os.environ.get("LLMTRAIN_GEMM_PP", "") == "all"
-                    else [t for t in os.environ.get("LLMTRAIN_GEMM_PP", "").split(",") if t in _GPP_SITES])
-
-
-def _gpp_ok(site: str, x, w, bias=None, *, kn: bool = False) -> bool:
-    if not (site in GEMM_PP and _on_gpu(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
-        return False
-    k, n = x.shape[1], (w.shape[1] if kn else w.shape[0])
-    return (k % 64 == 0 and n % 8 == 0 and x.stride(1) == 1 and w.stride(1) == 1 and x.stride(0) % 8 == 0
-            and w.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
-            and (bias is None or bias.data_ptr() % 8 == 0))
-
-
 _TUNED_BIAS_GEMMS: set[tuple[int, int, int]] | None = None
 
 
@@ -377,38 +421,31 @@ def _library_tuned_bias_gemm(m: int, n: int, k: int) -> bool:
 
 
 def linear_fwd(x, w, bias=None):
-    """``x @ w^T + bias`` (nn.Linear forward, bf16 out).  GPU: the ping-pong GEMM when enabled, the
-    fused MFMA GEMM with the bias in its epilogue where the shape allows and the library has no
-    measured solution for it, else hipBLASLt."""
-    if _gpp_ok("fwd", x, w, bias):
-        return hip_ops().gemm_pp(x, w, bias, 0)[0]
+    """``x @ w^T + bias`` (nn.Linear forward, bf16 out).  GPU: the fused MFMA GEMM with the bias in
+    its epilogue where the shape allows and the library has no measured solution for it, else
+    hipBLASLt."""
     if (_on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x, x.shape[1], w.shape[0], w, bias, op="fwd")
             and (_POLICY["deterministic"] or bias is None
                  or not _library_tuned_bias_gemm(x.shape[0], w.shape[0], x.shape[1]))):
         return _gemm_rows(x, w, False, 0, bias)[0]
-    return torch.mm(x, w.t()) if bias is None else torch.addmm(bias, x, w.t())
+    return _lib_mm(x, w.t(), bias, op="fwd")
 
 
 def linear_fwd_gelu(x, w, bias=None):
     """``u = x @ w^T + bias`` and ``g = gelu(u)`` (exact erf GELU of the bf16 ``u``, which the
     backward reads): on GPU the GELU rides in the GEMM epilogue, no separate pass over ``u``."""
-    if _gpp_ok("fwd_gelu", x, w, bias):
-        u, g = hip_ops().gemm_pp(x, w, bias, 1)
-        return u, g
     if _on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok(x, x.shape[1], w.shape[0], w, bias, op="fwd_gelu"):
         u, g = _gemm_rows(x, w, False, 1, bias)
         return u, g
-    u = torch.mm(x, w.t()) if bias is None else torch.addmm(bias, x, w.t())
+    u = _lib_mm(x, w.t(), bias, op="fc fwd")
     return u, gelu_fwd(u)
 
 
 def linear_dx(dy, w):
     """``dy @ w`` (data gradient of nn.Linear with weight ``w [out, in]``)."""
-    if _gpp_ok("dx", dy, w, kn=True):
-        return hip_ops().gemm_pp(dy, w, None, 0, True)[0]
     if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy, dy.shape[1], w.shape[1], w, op="dx"):
         return _gemm_rows(dy, w, True, 0)[0]
-    return torch.mm(dy, w)
+    return _lib_mm(dy, w, op="dX")
 
 
 # rows per launch of the LM-head GEMMs on the hand-written kernel: its buffer descriptors take
@@ -420,7 +457,7 @@ def head_logits(h, w):
     """``logits = h @ w^T`` for the vocab-padded LM head ``w [Vp, d]``: hipBLASLt, or row chunks
     of the hand-written GEMM when every GEMM runs on our kernels (deterministic mode)."""
     if not (_on_gpu(h) and _POLICY["gemm_all_ours"] and h.dtype == torch.bfloat16 and _fgemm_ok(h, h.shape[1], w.shape[0], w)):
-        return torch.mm(h, w.t())
+        return _lib_mm(h, w.t(), op="LM-head logits")
     out = torch.empty(h.shape[0], w.shape[0], dtype=h.dtype, device=h.device)
     for r0 in range(0, h.shape[0], _HEAD_ROWS):
         r1 = min(h.shape[0], r0 + _HEAD_ROWS)
@@ -453,11 +490,9 @@ def linear_dx_gelu_bwd(dy, w, u, dbias=None):
     """``du = (dy @ w) * gelu'(u)`` and ``dbias += colsum(du)``: the data gradient of the MLP
     projection fused with the GELU backward and the fc bias gradient (one GEMM epilogue on GPU
     instead of a GEMM plus a full read-modify pass over the [M, d_ff] activations)."""
-    if dbias is None and u.is_contiguous() and _gpp_ok("dx_gelu", dy, w, kn=True):
-        return hip_ops().gemm_pp(dy, w, None, 2, True, u)[0]
     if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok(dy, dy.shape[1], w.shape[1], w, u, op="dx_gelu"):
         return _gemm_rows(dy, w, True, 2, None, u, dbias)[0]
-    return gelu_bwd(torch.mm(dy, w), u, dbias)
+    return gelu_bwd(_lib_mm(dy, w, op="MLP-projection dX"), u, dbias)
 
 
 def linear_dx_attn(dy, w, att, seqlen: int, v_bias_grad=None, head_dim: int = 64):
@@ -468,9 +503,6 @@ def linear_dx_attn(dy, w, att, seqlen: int, v_bias_grad=None, head_dim: int = 64
     replacing the separate pass that re-read dO and O.  Returns ``(dO, delta)``; ``delta`` is None
     when the GEMM is not taken (the attention backward then computes it itself, and the caller
     must leave ``v_bias_grad`` to it)."""
-    if (v_bias_grad is None and head_dim == 64 and dy.shape[0] % seqlen == 0 and w.shape[1] % 64 == 0
-            and att.is_contiguous() and _gpp_ok("dx_attn", dy, w, kn=True)):
-        return tuple(hip_ops().gemm_pp(dy, w, None, 3, True, att, seqlen))
     if (
         _on_gpu(dy)
         and dy.dtype == torch.bfloat16
@@ -481,36 +513,21 @@ def linear_dx_attn(dy, w, att, seqlen: int, v_bias_grad=None, head_dim: int = 64
     ):
         return _gemm_rows(dy, w, True, 3, None, att, v_bias_grad, seqlen)
     if _on_gpu(dy) and head_dim != 64:
-        _det_fallback(f"attention out-projection dX at head_dim={head_dim}")
-    return torch.mm(dy, w), None
+        # the epilogue's row dots need 64-wide heads: a plain dX GEMM (fixed-order kernel where the
+        # shape allows, e.g. the reference presets' d = 256 / 384) and attn_bwd forms delta itself
+        return linear_dx(dy, w), None
+    return _lib_mm(dy, w, op="attention out-projection dX"), None
 
 
-# Weight-gradient kernel: "pp" = the ping-pong kernel (csrc/gemm_wgrad_pp.hip: 8 waves, 2 per
-# SIMD, slab epilogue, bias column sums fused), "r3" = the round-3 kernels (csrc/gemm_wgrad.hip).
-WGRAD_KERNEL = os.environ.get("LLMTRAIN_WGRAD_KERNEL", "pp")
-
-
-def wgrad_fuses_bias() -> bool:
-    """True when :func:`wgrad_accum` computes ``bias += colsum(dy)`` inside the GEMM kernel (the
-    engine then drops the separate bias column sums of the producing kernels)."""
-    return WGRAD_KERNEL == "pp"
-
-
-def wgrad_accum(dst, dy, x, *, bias=None, exclusive: bool = False) -> None:
+def wgrad_accum(dst, dy, x, *, bias=None) -> None:
     """``dst (fp32 [N, K]) += dy[M, N]^T @ x[M, K]`` and, with ``bias`` (fp32 ``[N]``),
     ``bias += colsum(dy)`` — the weight and bias gradients of an nn.Linear whose output gradient
-    is ``dy`` (``dy`` may be a column slice with a larger row stride).
-
-    GPU: the split-K MFMA GEMM (:data:`WGRAD_KERNEL`).  With the round-3 kernels ``exclusive``
-    (nothing runs beside this GEMM: the LM head's, on the main stream) selects the 512-register
-    software-pipelined variant, and the bias is a separate column-sum pass."""
+    is ``dy`` (``dy`` may be a column slice with a larger row stride).  GPU: the split-K MFMA GEMM
+    of csrc/gemm_wgrad_pp.hip with the bias column sums fused."""
     if _on_gpu(dst):
-        if WGRAD_KERNEL == "pp":
-            hip_ops().wgrad_gemm_pp(dy, x, dst, bias, 0, -1)
-            return
-        hip_ops().wgrad_gemm(dy, x, dst, 0, 0, 4 if exclusive else 0)
-    else:
-        dst.addmm_(dy.t().float(), x.float())
+        hip_ops().wgrad_gemm_pp(dy, x, dst, bias, 0, -1)
+        return
+    dst.addmm_(dy.t().float(), x.float())
     if bias is not None:
         colsum_accum(dy, bias)
 

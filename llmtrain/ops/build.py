@@ -32,7 +32,7 @@ OUT = Path(__file__).resolve().with_name("_llmtrain_hip.so")
 # of the release object when LLMTRAIN_DEBUG_KERNELS=1 (see llmtrain/ops/_ext.py)
 OUT_DEBUG = Path(__file__).resolve().with_name("_llmtrain_hip_debug.so")
 OBJDIR = REPO / "build" / "hip_obj"
-ARCH = os.environ.get("LLMTRAIN_OFFLOAD_ARCH", "gfx950")
+ARCH = "gfx950"  # MI355X (CDNA4) only
 
 
 def _hipcc() -> str:

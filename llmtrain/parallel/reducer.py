@@ -18,7 +18,12 @@ model in ``DistributedDataParallel`` at ``training/trainer.py:86-91``; SURVEY §
   rather than for NVSwitch;
 * **no buffer broadcasts** — the constant ``causal_mask`` buffers are never re-broadcast
   (SURVEY Q18); parameters are broadcast once from rank 0 at wrap time as a single flat tensor;
-* **no_sync()** — gradient accumulation micro-steps skip communication exactly like DDP.
+* **no_sync()** — gradient accumulation micro-steps skip communication exactly like DDP;
+* **comm stream at high priority** — RCCL's workgroups are dispatched ahead of the compute
+  stream's queued GEMM tiles instead of waiting for a whole kernel's worth of them to drain;
+* **bucket-wise gradient norm** — as soon as a bucket's all-reduce is done, its squared L2 norm is
+  summed on the comm stream (:meth:`grad_sumsq`), so after the backward the clip coefficient needs
+  only the last (tied-embedding) bucket's partial instead of a pass over every gradient.
 """
 
 from __future__ import annotations
@@ -106,8 +111,16 @@ class FlatDataParallel(nn.Module):
         self._exposed_hist: deque[tuple[Any, Any] | float] = deque(maxlen=256)
         self._trace: list[list[Any]] = []  # this step's [bucket, ready, start, end] rows
         self._trace_hist: deque[list[list[Any]]] = deque(maxlen=64)
-        # GPU: collectives are issued from a dedicated comm stream (see _launch)
-        self._comm = torch.cuda.Stream(device=self._store.grad.device) if self._store.grad.is_cuda else None
+        # GPU: collectives are issued from a dedicated comm stream (see _launch), created at the highest
+        # priority the device offers: with one compute stream holding every CU, a default-priority
+        # stream's RCCL workgroups would queue behind the GEMM tiles already waiting for a CU
+        self._comm = (
+            torch.cuda.Stream(device=self._store.grad.device, priority=torch.cuda.Stream.priority_range()[1])
+            if self._store.grad.is_cuda else None
+        )
+        # squared L2 norm of each bucket's reduced gradient (written on the comm stream / at finish)
+        self._sq = torch.zeros(len(self.buckets), dtype=torch.float32, device=self._store.grad.device)
+        self._sq_ready = False
         engine.grad_ready = self._on_segment_ready
         if broadcast_parameters and self.world_size > 1:
             with torch.no_grad():
@@ -149,6 +162,7 @@ class FlatDataParallel(nn.Module):
                 raise RuntimeError("previous gradient all-reduce was not finished")
             self._remaining = [len(b.segments) for b in self.buckets]
             self._armed = True
+            self._sq_ready = False
 
     def _on_segment_ready(self, segment: str) -> None:
         if not (self._sync and self._armed):
@@ -189,10 +203,23 @@ class FlatDataParallel(nn.Module):
                 work.wait()  # RCCL: the comm stream waits for the collective (the host does not)
                 if staged is not None:
                     view.copy_(staged)
+                self._bucket_sumsq(bucket, view)
                 end.record()
                 work = None
         self._works.append((bucket, work, staged))
         self._trace.append([bucket, ready, start, end])
+
+    def _bucket_sumsq(self, bucket: Bucket, view: torch.Tensor) -> None:
+        """This bucket's squared norm into its slot, on the stream that finished its reduction."""
+        from llmtrain import ops
+
+        self._sq[bucket.index : bucket.index + 1].copy_(ops.sumsq(view).reshape(1))
+
+    def grad_sumsq(self) -> torch.Tensor | None:
+        """Squared global L2 norm of the reduced gradients of the last synchronised step (device
+        scalar, after :meth:`finish_gradient_sync`), summed from the per-bucket partials in bucket
+        order; ``None`` when the last step did not synchronise (accumulation micro-steps)."""
+        return self._sq.sum() if self._sq_ready else None
 
     def _staged_dtype(self, view: torch.Tensor) -> bool:
         return self.reduce_dtype is not None and self.reduce_dtype != view.dtype
@@ -225,6 +252,7 @@ class FlatDataParallel(nn.Module):
                 view.copy_(staged)
             if not self._avg_native:
                 view.div_(self.world_size)
+            self._bucket_sumsq(bucket, view)
             if on_gpu:  # gloo on GPU tensors (a rehearsal): completion seen at this wait, an upper bound
                 self._trace[i][3].record()
             else:
@@ -240,6 +268,7 @@ class FlatDataParallel(nn.Module):
         self._trace = []
         self._works.clear()
         self._armed = False
+        self._sq_ready = True
 
     def bucket_timeline(self) -> list[list[dict[str, float]]]:
         """Per synchronised step since the last call (oldest first, at most 64), per bucket:

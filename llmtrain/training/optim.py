@@ -186,9 +186,13 @@ class FusedAdamW(torch.optim.Optimizer):
         self.store.mark_shadow_synced()
 
 
-def fused_clip_coef(store: Any, max_norm: float) -> tuple[torch.Tensor, torch.Tensor]:
-    """Global grad L2 norm and ``min(1, max_norm / (norm + 1e-6))``, both as device scalars."""
-    total = torch.sqrt(ops.sumsq(store.grad))
+def fused_clip_coef(
+    store: Any, max_norm: float, *, sumsq: torch.Tensor | None = None
+) -> tuple[torch.Tensor, torch.Tensor]:
+    """Global grad L2 norm and ``min(1, max_norm / (norm + 1e-6))``, both as device scalars.
+    ``sumsq``: the squared norm already summed elsewhere (the data-parallel reducer's per-bucket
+    partials, :meth:`FlatDataParallel.grad_sumsq`) instead of a pass over ``store.grad``."""
+    total = torch.sqrt(ops.sumsq(store.grad) if sumsq is None else sumsq)
     coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
     return total, coef
 

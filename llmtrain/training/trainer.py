@@ -184,12 +184,6 @@ class Trainer:
         self._policy = policy
         self._device = self._policy.device
         self.tuned_gemms = enable_tuned_gemms(self._device)  # shipped hipBLASLt solution table (GPU)
-        if self._device.type == "cuda":
-            # run.deterministic: fixed-order reductions in every HIP kernel (bitwise-reproducible
-            # steps and resumes); false = the split-K / scatter atomics of the fast path
-            from llmtrain import ops
-
-            ops.set_deterministic(cfg.run.deterministic)
         model = model.to(self._device)
         if self._policy.use_fused:
             model.prepare_runtime(compute_dtype=self._policy.compute_dtype)
@@ -428,7 +422,10 @@ class Trainer:
             finish()
         max_norm = self._cfg.trainer.max_grad_norm
         if isinstance(self._optimizer, FusedAdamW):
-            norm, coef = fused_clip_coef(self._optimizer.store, max_norm)
+            # data parallel: the reducer summed each bucket's squared norm as its all-reduce finished
+            bucket_sumsq = getattr(self._model, "grad_sumsq", None)
+            sq = bucket_sumsq() if bucket_sumsq is not None else None
+            norm, coef = fused_clip_coef(self._optimizer.store, max_norm, sumsq=sq)
             self._optimizer.step(grad_scale=coef)
         else:
             norm = torch.nn.utils.clip_grad_norm_(self._model.parameters(), max_norm)
@@ -440,12 +437,27 @@ class Trainer:
         """Endless iterator over this trainer's training DataLoader."""
         return _Batches(self._train_loader)
 
+    def kernel_policy(self) -> contextlib.AbstractContextManager[Any]:
+        """``run.deterministic`` for the HIP kernels (fixed-order reductions: bitwise-reproducible
+        steps and resumes; false = the split-K / scatter atomics of the fast path), scoped to this
+        trainer's own work: :meth:`fit` and :meth:`train_step` run under it, and the process-wide
+        policy they found is restored when they return, so it never leaks into another trainer."""
+        if self._device.type != "cuda":
+            return contextlib.nullcontext()
+        from llmtrain import ops
+
+        return ops.kernel_policy(self._cfg.run.deterministic)
+
     def train_step(self, batches: _Batches) -> tuple[torch.Tensor, int]:
         """One optimizer step (all micro-batches, gradient sync, clip, AdamW, LR schedule).
 
         Returns the step's mean loss as a 0-d DEVICE tensor (no host sync) and its token count.
         ``bench.py`` times exactly this method.
         """
+        with self.kernel_policy():
+            return self._train_step(batches)
+
+    def _train_step(self, batches: _Batches) -> tuple[torch.Tensor, int]:
         accum = self._cfg.trainer.grad_accum_steps
         if self._graphed is not None:  # trainer.extra.cuda_graph: replay the captured step
             host = [_drop_dense_mask(batches.next()) for _ in range(accum)]
@@ -513,7 +525,8 @@ class Trainer:
         """Train to ``max_steps``; an asynchronous checkpoint still being written is flushed to disk
         before this returns or re-raises (a crash mid-run keeps the last complete checkpoint)."""
         try:
-            result = self._fit(max_steps_override=max_steps_override, resume_from=resume_from)
+            with self.kernel_policy():
+                result = self._fit(max_steps_override=max_steps_override, resume_from=resume_from)
         except BaseException:
             if self._ckpt_mgr is not None:
                 try:

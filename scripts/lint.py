@@ -11,7 +11,10 @@ offline MI355X image too:
   re-export modules and names listed in ``__all__``);
 * no line over 130 (Python) / 140 (HIP, C++) characters, no trailing whitespace, no tab indentation;
 * HIP sources: no CUDA compatibility layers (``__HIP_PLATFORM_*`` dual paths, ``cuda_runtime``
-  includes, hipify markers) — the kernels are written for gfx950 directly.
+  includes, hipify markers) — the kernels are written for gfx950 directly;
+* environment knobs: every ``LLMTRAIN_*`` / ``LLMT_*`` variable read in ``llmtrain/``, ``csrc/`` or
+  ``bench.py`` is listed in ``llmtrain/runtime/knobs.py`` (at most ``MAX_KNOBS``), none is read
+  from C++, and the knob table of ``docs/debugging.md`` lists exactly those.
 
 Exit status 1 when anything is found (the findings are printed as ``path:line: message``).
 """
@@ -118,6 +121,37 @@ def check_hip(path: Path) -> list[str]:
     return findings
 
 
+KNOB_READ = re.compile(r"""(?:environ(?:\.get)?\(|environ\[|getenv\()\s*["'](LLMT[A-Z0-9_]*)""")
+
+
+def _knob_registry() -> tuple[dict[str, object], int]:
+    """KNOBS / MAX_KNOBS of llmtrain/runtime/knobs.py, read without importing the package (torch)."""
+    ns: dict[str, object] = {}
+    exec(compile((ROOT / "llmtrain" / "runtime" / "knobs.py").read_text(), "knobs.py", "exec"), ns)
+    return ns["KNOBS"], ns["MAX_KNOBS"]  # type: ignore[return-value]
+
+
+def check_knobs() -> list[str]:
+    knobs, cap = _knob_registry()
+    findings = []
+    if len(knobs) > cap:
+        findings.append(f"llmtrain/runtime/knobs.py: {len(knobs)} knobs > {cap}")
+    files = sorted((ROOT / "llmtrain").rglob("*.py")) + [ROOT / "bench.py"]
+    files += [f for f in sorted((ROOT / "csrc").glob("*")) if f.suffix in (".hip", ".h", ".cpp")]
+    for f in files:
+        rel = f.relative_to(ROOT)
+        for i, line in enumerate(f.read_text().splitlines(), 1):
+            if f.suffix != ".py" and "getenv" in line:
+                findings.append(f"{rel}:{i}: environment read in native code (knobs live in Python)")
+            for name in KNOB_READ.findall(line):
+                if name not in knobs:
+                    findings.append(f"{rel}:{i}: knob {name} is not in llmtrain/runtime/knobs.py")
+    documented = set(re.findall(r"^\| `(LLMTRAIN_[A-Z0-9_]+)` \|", (ROOT / "docs" / "debugging.md").read_text(), re.M))
+    if documented != set(knobs):
+        findings.append(f"docs/debugging.md: knob table {sorted(documented)} != knobs.py {sorted(knobs)}")
+    return findings
+
+
 def run_external() -> int:
     rc = 0
     if shutil.which("ruff") or importlib.util.find_spec("ruff"):
@@ -138,6 +172,7 @@ def main() -> int:
     for f in sorted((ROOT / "csrc").glob("*")) + sorted((ROOT / "bench" / "native").glob("*.cpp")):
         if f.suffix in (".hip", ".h", ".cpp"):
             findings += check_hip(f)
+    findings += check_knobs()
     for line in findings:
         print(line)
     external = run_external() if "--builtin-only" not in sys.argv else 0

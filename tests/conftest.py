@@ -38,6 +38,28 @@ def minimal_payload(**overrides: object) -> dict[str, object]:
     return payload
 
 
+_POLICY_ENV = ("LLMTRAIN_DET_SCHEDULE", "LLMTRAIN_WGRAD_STREAM")
+
+
+@pytest.fixture(autouse=True)
+def _isolated_kernel_policy():
+    """Every test starts and ends with the same process-wide kernel policy (``ops._POLICY``, the
+    C++ deterministic flag and the environment knobs that feed them): a test that switches
+    deterministic mode, directly or through a Trainer, cannot change the routing of a later test —
+    in particular the bench-shape step test always runs the routing it names."""
+    from llmtrain import ops
+
+    state = ops.policy_state()
+    env = {k: os.environ.get(k) for k in _POLICY_ENV}
+    yield
+    ops.restore_policy(state)
+    for k, v in env.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+
+
 @pytest.fixture
 def in_tmp(tmp_path: Path, monkeypatch: pytest.MonkeyPatch) -> Path:
     monkeypatch.chdir(tmp_path)

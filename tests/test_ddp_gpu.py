@@ -58,6 +58,14 @@ def test_flat_ddp_over_rccl_matches_single_process(nccl_world):
     diff = (base.flat_store.grad - solo.flat_store.grad).abs().max().item()
     scale = solo.flat_store.grad.abs().max().item()
     assert diff <= 1e-3 * scale  # only float-atomic ordering differs
+    # the comm stream outranks the compute stream, and the bucket-wise norm (summed on it as each
+    # RCCL all-reduce finished) equals the one-pass global norm of the reduced buffer
+    assert ddp._comm.priority == torch.cuda.Stream.priority_range()[1] < torch.cuda.current_stream().priority
+    from llmtrain.training.optim import fused_clip_coef
+
+    norm_b, _ = fused_clip_coef(base.flat_store, 1.0, sumsq=ddp.grad_sumsq())
+    norm_g, _ = fused_clip_coef(base.flat_store, 1.0)
+    torch.testing.assert_close(norm_b, norm_g, rtol=1e-5, atol=0.0)
 
 
 def test_flat_ddp_rccl_bf16_buckets_stream_order_and_timeline(nccl_world):

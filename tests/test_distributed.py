@@ -128,10 +128,25 @@ def _reducer_worker(rank: int, world: int, port: int, out_dir: str) -> None:
         (ddp.fused_loss(batches[0], batches[0]) / 2).backward()
     (ddp.fused_loss(batches[1], batches[1]) / 2).backward()
     ddp.finish_gradient_sync()
+    # bucket-wise squared norms (summed as each bucket's reduction finished) == one pass over the
+    # reduced flat gradient, which is what fused_clip_coef computes without a reducer
+    from llmtrain.training.optim import fused_clip_coef
+
+    sq = ddp.grad_sumsq()
+    assert sq is not None
+    norm_b, coef_b = fused_clip_coef(model.flat_store, 0.5, sumsq=sq)
+    norm_g, coef_g = fused_clip_coef(model.flat_store, 0.5)
+    torch.testing.assert_close(norm_b, norm_g, rtol=1e-6, atol=0.0)
+    torch.testing.assert_close(coef_b, coef_g, rtol=1e-6, atol=0.0)
     torch.save(
         {"params": model.flat_store.master.clone(), "grad": model.flat_store.grad.clone(), "batches": batches},
         Path(out_dir) / f"rank{rank}.pt",
     )
+    with ddp.no_sync():  # an accumulation micro-step has no synchronised gradients yet
+        ddp.fused_loss(batches[0], batches[0]).backward()
+    assert ddp.grad_sumsq() is not None  # still the last synchronised step's until the next arm
+    ddp.fused_loss(batches[0], batches[0])  # arms the next synchronised step ...
+    assert ddp.grad_sumsq() is None  # ... whose norm is not known before its backward
     dist.destroy_process_group()
 
 

@@ -171,12 +171,17 @@ def test_fused_engine_mid_run_resume(gpu_device, tmp_path, dropout):
     assert abs(resumed.final_loss - full.final_loss) <= 1e-5 * abs(full.final_loss)
 
 
-def test_fused_step_at_benchmark_shape(gpu_device):
+@pytest.mark.parametrize("deterministic", [False, True])
+def test_fused_step_at_benchmark_shape(gpu_device, deterministic):
     """One fused step with the benchmark's exact routing — micro-batch 128 x 1024 tokens, d 768,
     12 heads, V 50257, so every GEMM takes its M = 131072 path (hipBLASLt above the fused-GEMM size
     cap, the GELU / attention dX epilogues at any size, the per-(b, h) fp32-dQ attention backward at
     B*H = 1536, the LM head's 50304-wide logits) — against fp32 autograd of the module path, with 2
-    layers instead of 12.  Bound: per-parameter relative gradient error (bf16 compute)."""
+    layers instead of 12.  ``deterministic=False`` is the bench's fast path (split-K atomics, library
+    forward / dX GEMMs: asserted from the kernel trace); ``True`` the serial deterministic schedule.
+    Bound: per-parameter relative gradient error (bf16 compute)."""
+    from llmtrain import ops
+
     torch.manual_seed(0)
     V, T, B = 50257, 1024, 128
     ref_model = GPT(vocab_size=V, block_size=T, d_model=768, n_layers=2, n_heads=12, d_ff=3072, dropout=0.0)
@@ -205,9 +210,20 @@ def test_fused_step_at_benchmark_shape(gpu_device):
 
     engine = fused.prepare_runtime(compute_dtype=torch.bfloat16)
     engine.store.zero_grad()
-    loss = fused.fused_loss(ids, labels)
-    loss.backward()
-    torch.cuda.synchronize()
+    acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
+    with ops.kernel_policy(deterministic), torch.profiler.profile(activities=acts) as prof:
+        assert ops._POLICY["deterministic"] is deterministic and ops._POLICY["single_stream"] is deterministic
+        assert not ops._POLICY["gemm_all_ours"]
+        assert torch.ops.llmtrain_hip.get_deterministic() is deterministic
+        loss = fused.fused_loss(ids, labels)
+        loss.backward()
+        torch.cuda.synchronize()
+    kernels = {e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA}
+    ours = ("wgrad_pp_kernel", "attn_fwd_kernel", "attn_bwd", "ce_fwd_bwd", "gemm_fused_kernel")
+    for k in ours:
+        assert any(k in n for n in kernels), f"{k} missing from the step's kernel trace"
+    # the forward / dX GEMMs above the fused-GEMM size cap run on hipBLASLt (Tensile "Cijk_" kernels)
+    assert any(n.startswith("Cijk_") for n in kernels), sorted(kernels)[:40]
     assert abs(loss.item() - loss_ref) < 1e-2 * abs(loss_ref)
     worst, worst_name = 0.0, ""
     for name, p in fused.named_parameters():
@@ -216,4 +232,4 @@ def test_fused_step_at_benchmark_shape(gpu_device):
         if rel > worst:
             worst, worst_name = rel, name
         assert rel < 3e-2, f"{name}: relative grad error {rel:.3e}"
-    print(f"worst relative grad error {worst:.3e} ({worst_name})")
+    print(f"deterministic={deterministic}: worst relative grad error {worst:.3e} ({worst_name})")

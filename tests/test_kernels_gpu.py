@@ -46,8 +46,8 @@ def test_add_layernorm_fwd(gpu_device, M, d, with_delta):
 @pytest.mark.parametrize("M,d", [(4096, 768), (4099, 768), (100, 64), (777, 384), (513, 1600)])
 @pytest.mark.parametrize("with_proj,lowp", [(True, True), (False, False), (False, True)])
 def test_layernorm_bwd(gpu_device, M, d, with_proj, lowp):
-    """Every LayerNorm-backward variant (LLMT_LN_BWD_LEAN picks the kernel for d <= 768; the
-    GPU tier is also run under each setting) against the fp32 reference: with / without the
+    """Every LayerNorm-backward variant (the lean kernel for d <= 768, the general one above)
+    against the fp32 reference: with / without the
     projection-bias column sum and the bf16 copy, odd row counts (dead rows of a 2-row wave)."""
     g = torch.Generator(device="cpu").manual_seed(7)
     x = torch.randn(M, d, generator=g).to(gpu_device)
@@ -239,29 +239,6 @@ def test_layernorm_bwd_deferred_params_batched(gpu_device, M, d):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("tile", [0, 128, 256])
-@pytest.mark.parametrize("M,N,K,lda", [(4096, 768, 768, 768), (2048, 2304, 768, 2304), (1000, 200, 72, 200),
-                                        (3000, 1000, 768, 1024), (2080, 1600, 4800, 1600),
-                                        (1500, 1001, 768, 1024)])  # odd N in a padded row (LM head)
-def test_wgrad_gemm(gpu_device, M, N, K, lda, tile):
-    """Split-K MFMA weight-gradient GEMM accumulates dY^T X into an existing fp32 buffer, for both
-    tile configurations and the cost-model choice; also with a column-slice dY (row stride
-    lda > N, like the vocab-padded logits) and GPT-2 XL widths that are not tile multiples."""
-    g = torch.Generator(device="cpu").manual_seed(M + N + K)
-    dy_full = torch.randn(M, lda, generator=g).to(gpu_device, torch.bfloat16)
-    dy = dy_full[:, :N]
-    x = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)
-    c = torch.randn(N, K, generator=g).to(gpu_device)
-    want = c + dy.float().t() @ x.float()
-    hip().wgrad_gemm(dy, x, c, 0, tile)
-    scale = want.abs().max().item()
-    _close(c, want, 1e-3 * scale, 1e-3, "wgrad")
-    # an explicit split also works and is additive
-    c2 = torch.zeros(N, K, device=gpu_device)
-    hip().wgrad_gemm(dy, x, c2, 3, tile)
-    _close(c2, dy.float().t() @ x.float(), 1e-3 * scale, 1e-3, "wgrad split=3")
-
-
 @pytest.mark.parametrize("mode", [-1, 0, 2])
 @pytest.mark.parametrize("M,N,K,lda", [(4096, 768, 768, 768), (2048, 2304, 768, 2304), (1000, 200, 72, 200),
                                         (3000, 1000, 768, 1024), (2080, 1600, 4800, 1600),
@@ -340,52 +317,6 @@ def test_gemm_fused_bias_gelu(gpu_device, M, N, K, b_kn):
     _close(u, u_ref, 2e-2, 1e-2, "u")
     # GELU is applied to the bf16 pre-activation the backward will see
     _close(gl, torch.nn.functional.gelu(u.float()), 1e-2, 1e-2, "gelu(u)")
-
-
-# ---- ping-pong forward GEMM (csrc/gemm_pp.hip) ------------------------------------------------
-GPP_SHAPES = [(4096, 2304, 768), (513, 768, 3072), (1000, 200, 256), (300, 776, 128), (64, 50304, 768),
-              (131072, 768, 768)]  # bench M; ragged M / N; N past one tile row; the LM head's width
-
-
-@pytest.mark.parametrize("M,N,K", GPP_SHAPES)
-def test_gemm_pp_bias_gelu(gpu_device, M, N, K):
-    a, w, _, bias = _gemm_operands(M, N, K, False, gpu_device, 7 * M + N)
-    out, none = hip().gemm_pp(a, w, bias, 0)
-    assert none is None
-    ref = a.float() @ w.float().t() + bias.float()
-    _close(out, ref, 2e-2, 1e-2, "gemm_pp+bias")
-    out_nb, _ = hip().gemm_pp(a, w, None, 0)
-    _close(out_nb, a.float() @ w.float().t(), 2e-2, 1e-2, "gemm_pp")
-    u, gl = hip().gemm_pp(a, w, bias, 1)
-    assert torch.equal(u, out), "epilogue 1's pre-activation differs from epilogue 0"
-    _close(gl, torch.nn.functional.gelu(u.float()), 1e-2, 1e-2, "gelu(u)")
-    again, _ = hip().gemm_pp(a, w, bias, 0)
-    assert torch.equal(out, again), "gemm_pp is not deterministic"
-
-
-GPP_DX_SHAPES = [(4096, 768, 3072), (1000, 3072, 768), (2048, 768, 768), (300, 776, 128)]
-
-
-@pytest.mark.parametrize("M,N,K", GPP_DX_SHAPES)
-def test_gemm_pp_dx_epilogues(gpu_device, M, N, K):
-    """Data-gradient layout (dX = dY W, W [K, N]): plain, GELU backward (du = acc * gelu'(u)) and,
-    for whole 1024-token sequences, the attention row constants delta = per-head dO . O."""
-    g = torch.Generator(device="cpu").manual_seed(M + N)
-    dy = (torch.randn(M, K, generator=g) / math.sqrt(K)).to(gpu_device, torch.bfloat16)
-    w = torch.randn(K, N, generator=g).to(gpu_device, torch.bfloat16)
-    u = torch.randn(M, N, generator=g).to(gpu_device, torch.bfloat16)
-    ref = dy.float() @ w.float()
-    out, _ = hip().gemm_pp(dy, w, None, 0, True)
-    _close(out, ref, 2e-2, 1e-2, "gemm_pp kn")
-    du, _ = hip().gemm_pp(dy, w, None, 2, True, u)
-    x = u.float().requires_grad_(True)
-    torch.nn.functional.gelu(x).backward(torch.ones_like(x))
-    _close(du, out.float() * x.grad, 3e-2, 2e-2, "gemm_pp kn gelu'")
-    if M % 1024 == 0 and N % 64 == 0:
-        d_o, delta = hip().gemm_pp(dy, w, None, 3, True, u, 1024)
-        assert torch.equal(d_o, out)
-        dref = (d_o.float() * u.float()).view(M // 1024, 1024, N // 64, 64).sum(-1).permute(0, 2, 1)
-        _close(delta, dref, 1e-3, 1e-4, "gemm_pp delta")
 
 
 @pytest.mark.parametrize("M,N,K", GEMM_SHAPES)

@@ -15,6 +15,7 @@
 #   parity[:ARGS]      bench/parity.py ARGS
 #   repeat[:M]         bench/repeat_check.py M
 #   ab:ENVA|ENVB[:ARGS] same-box interleaved bench.py A/B (scripts/abn.sh)
+#   wpp:ARGS           bench/wgrad_pp.py ARGS (weight-gradient GEMM numerics / timing)
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -66,6 +67,7 @@ for step in "$@"; do
     ab) envs=${arg%%:*}; rest=""; [[ "$arg" == *:* ]] && rest=${arg#*:}
       IFS='|' read -r -a E <<< "$envs"
       run ab 1000 bash scripts/abn.sh "${E[@]}" -- ${rest//,/ } ;;
+    wpp) run "wpp_${arg%%,*}" 300 python -u bench/wgrad_pp.py ${arg//,/ } ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

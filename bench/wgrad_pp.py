@@ -89,7 +89,7 @@ def time_shapes(model: str, M: int, only: str = "") -> None:
             "pp_slab_bias": lambda: ops.wgrad_gemm_pp(dy, x, acc, bias, 0, 0),
         }
         for label, fn in variants.items():
-            if only and label not in only.split(","):
+            if only and label not in only.replace("+", ",").split(","):
                 continue
             ms = timeit(fn)
             print(json.dumps({"model": model, "M": M, "gemm": name, "variant": label, "ms": round(ms, 4),

@@ -541,6 +541,7 @@ hipError_t plan_wgrad_pp(int lda, int ldb, int M, int N, int K, int split, int m
   // W4 keeps its accumulators in AGPRs through the slab epilogue only (a direct C epilogue made the
   // register allocator spill): always slabs, also for split 1
   p = plan_pp(M, N, K, split, det || variant == 1 ? 0 : mode, device_cu_count(), 1);
+  if (variant == 1) p.mode = 0;  // (the plan picks the direct C epilogue, mode 1, for split 1)
   p.slabs = p.mode == 0 && (p.split > 1 || variant == 1);
   return hipSuccess;
 }
@@ -573,7 +574,8 @@ hipError_t launch_wgrad_pp(const void* dy, int lda, const void* x, int ldb, floa
   hipLaunchKernelGGL(KERNEL, dim3(nwg), dim3(THREADS), 0, stream, (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, \
                      c, ldc, M, N, K, p.tiles, p.tiles_k, p.m_chunk, p.split, nwg, slab, bias_parts)
   if (variant == 1) {
-    LLMT_WPP_LAUNCH(wpp::wgrad_w4_kernel, 256);  // slabs only (plan_wgrad_pp)
+    if (!slabs || slab == nullptr) return hipErrorInvalidValue;  // W4 has no other epilogue
+    LLMT_WPP_LAUNCH(wpp::wgrad_w4_kernel, 256);
   } else {
     if (m == 0) LLMT_WPP_LAUNCH(wpp::wgrad_pp_kernel<0>, wpp::kThreads);
     else if (m == 1) LLMT_WPP_LAUNCH(wpp::wgrad_pp_kernel<1>, wpp::kThreads);

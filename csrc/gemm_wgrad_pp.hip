@@ -284,15 +284,17 @@ __device__ __forceinline__ void mfma4(f32x4v& c0, f32x4v& c1, f32x4v& c2, f32x4v
 // the 8-wave 128 x 64 ping-pong above: 1/3 fewer LDS bytes per FLOP, the LDS budget that kept that
 // schedule at ~1.1 PF (docs/round4.md section 1).  With no partner wave to cover its loads, each
 // wave software-pipelines itself: stage s's 64 MFMAs run from registers while the same wave reads
-// stage s+1's fragments (double-buffered: 2 x 64 VGPRs), writes stage s+2 into the LDS slot stage s
-// came from and loads stage s+3, the four kinds of work interleaved in 16 pinned groups of 4 MFMAs
-// (sched_barrier), one barrier per stage.  Two 32 KiB slots suffice: a slot is rewritten one stage
-// after its fragments were read, and every read of it finished before the barrier between.
+// stage s+1's fragments (A fragments re-read in place after their last use, B double-buffered),
+// writes stage s+2 into its LDS slot and loads stage s+4 (two register sets: a load has two stages
+// to land), the four kinds of work interleaved in 16 pinned groups of 4 MFMAs (sched_barrier), one
+// barrier per stage.  Four 32 KiB slots: a slot is rewritten two stages after its fragments were
+// read, so the barrier only waits for this wave's writes (counted lgkmcnt) and the fragment reads
+// of the stage's last groups stay in flight across it (a 2-slot ring exposed them at every stage).
 __global__ __launch_bounds__(256, 1) void wgrad_w4_kernel(
     const bf16_raw* __restrict__ A, int lda, const bf16_raw* __restrict__ B, int ldb, float* __restrict__ C,
     int ldc, int M, int N, int K, int tiles, int tiles_k, int m_chunk, int split, int nwg, float* __restrict__ slab,
     float* __restrict__ bias_slab) {
-  __shared__ __attribute__((aligned(16))) bf16_raw smem[2 * SLOT / 2];
+  __shared__ __attribute__((aligned(16))) bf16_raw smem[4 * SLOT / 2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wn = wave >> 1, wk = wave & 1;
@@ -342,9 +344,9 @@ __global__ __launch_bounds__(256, 1) void wgrad_w4_kernel(
 
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
-  u32x4 R[8];  // staged stage: A pieces 0-3, B pieces 4-7
+  u32x4 R0[8], R1[8];  // staged stages (even, odd): A pieces 0-3, B pieces 4-7
   // unconditional loads: a stage past the chunk has a zero-record descriptor and loads zeros
-  auto load_piece = [&](int st, int j) {
+  auto load_piece = [&](u32x4 (&R)[8], int st, int j) {
     const int r0 = st * BR, nr = max(0, min(BR, rows - r0));
     if (j < 4) {
       const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(A + (long)(m_begin + r0) * lda, nr * lda * 2);
@@ -354,7 +356,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_w4_kernel(
       R[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, vob[j - 4], 0, 0));
     }
   };
-  auto write_piece = [&](int slot, int j) {
+  auto write_piece = [&](const u32x4 (&R)[8], int slot, int j) {
     const unsigned a = lds + slot * SLOT + (j < 4 ? 0 : IMG) + wave * 4096 + (j & 3) * 1024 + 16 * lane;
     *(lds_u32x4*)(size_t)a = R[j];
   };
@@ -362,31 +364,33 @@ __global__ __launch_bounds__(256, 1) void wgrad_w4_kernel(
     return tr_read(lds + slot * SLOT + (f < 8 ? ao[f] : bo[f - 8]));
   };
 
-  // prologue: stages 0 and 1 in slots 0 and 1, stage 2 loading, stage 0's fragments in registers
+  // prologue: stages 0 and 1 in slots 0 and 1, stages 2 and 3 loading, stage 0's fragments in
+  // registers
   bf16x8 fa[8], fb[8], gb[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) load_piece(0, j);
+  for (int j = 0; j < 8; ++j) load_piece(R0, 0, j);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) write_piece(0, j);
+  for (int j = 0; j < 8; ++j) load_piece(R1, 1, j);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) load_piece(1, j);
+  for (int j = 0; j < 8; ++j) write_piece(R0, 0, j);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) write_piece(1, j);
+  for (int j = 0; j < 8; ++j) write_piece(R1, 1, j);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) load_piece(2, j);
+  for (int j = 0; j < 8; ++j) load_piece(R0, 2, j);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) load_piece(R1, 3, j);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
   for (int f = 0; f < 8; ++f) fa[f] = read_frag(0, f);
 #pragma unroll
   for (int f = 0; f < 8; ++f) fb[f] = read_frag(0, 8 + f);
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
   // one stage: MFMAs on (fa, cb) = stage st, A-fragment-major, so A fragment i is dead after
   // groups 2i and 2i+1 and its successor of stage st+1 is read into the same registers (single
-  // buffer); the B fragments are used by every group and double-buffered (cb -> nb).  Slot `rs` holds
-  // stage st+1; stage st+2 (in R) goes into slot `ws` = the slot stage st was read from; stage
-  // st+3 is loaded into R.
-  auto stage = [&](int st, int rs, int ws, bf16x8 (&cb)[8], bf16x8 (&nb)[8]) {
+  // buffer); the B fragments are used by every group and double-buffered (cb -> nb).  Stage st+1
+  // is in slot (st+1) % 4; stage st+2 (in R, loaded two stages ago) goes into slot (st+2) % 4, whose
+  // last reads (stage st-2's fragments) ended two barriers ago; stage st+4 is loaded into R.
+  auto stage = [&](int st, int rs, int ws, u32x4 (&R)[8], bf16x8 (&cb)[8], bf16x8 (&nb)[8]) {
 #pragma unroll
     for (int grp = 0; grp < 16; ++grp) {
       const int i = grp >> 1, j0 = 4 * (grp & 1);
@@ -396,26 +400,32 @@ __global__ __launch_bounds__(256, 1) void wgrad_w4_kernel(
         asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(bacc[i]) : "v"(fa[i]), "v"(ones));
       if (grp & 1) fa[i] = read_frag(rs, i);  // A fragment i of stage st+1 (its last use was above)
       else nb[grp >> 1] = read_frag(rs, 8 + (grp >> 1));
-      if (grp >= 4 && grp < 8) {  // stage st+2 into the free slot
-        write_piece(ws, 2 * (grp - 4));
-        write_piece(ws, 2 * (grp - 4) + 1);
+      if (grp >= 8 && grp < 12) {  // stage st+2 into its slot
+        write_piece(R, ws, 2 * (grp - 8));
+        write_piece(R, ws, 2 * (grp - 8) + 1);
       }
-      if (grp >= 8 && grp < 12) {  // stage st+3 into the registers just written out
-        load_piece(st + 3, 2 * (grp - 8));
-        load_piece(st + 3, 2 * (grp - 8) + 1);
+      if (grp >= 12) {  // stage st+4 into the registers just written out
+        load_piece(R, st + 4, 2 * (grp - 12));
+        load_piece(R, st + 4, 2 * (grp - 12) + 1);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // this wave's writes of stage st+2 have landed (the 8 fragment reads of groups 12-15, issued
+    // after them, may still be in flight: the slot they read is rewritten two stages later), then
+    // the barrier
+    asm volatile("s_waitcnt lgkmcnt(8)\n\ts_barrier" ::: "memory");
   };
-  // pairs of unconditional stages (slots and B register sets compile-time in each); an odd last stage
-  // is padded with a stage of zeros
-  for (int s0 = 0; s0 < nst; s0 += 2) {
-    stage(s0, 1, 0, fb, gb);
-    stage(s0 + 1, 0, 1, gb, fb);
+  // groups of four unconditional stages (slots, register sets and B buffers compile-time in each);
+  // the stage count is padded with stages of zeros to a multiple of 4
+  for (int s0 = 0; s0 < nst; s0 += 4) {
+    stage(s0, 1, 2, R0, fb, gb);
+    stage(s0 + 1, 2, 3, R1, gb, fb);
+    stage(s0 + 2, 3, 0, R0, fb, gb);
+    stage(s0 + 3, 0, 1, R1, gb, fb);
   }
   asm volatile("s_nop 15" ::: "memory");  // the last MFMAs' results settle before compiler code reads them
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the loads past the last stage land before exit
+  // the loads and fragment reads past the last stage land before the epilogue (and the exit)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 
   // ---- epilogue.  Accumulator (i, j) register r of lane l: n = n0 + 128 wn + 16 ((i + 4 wk) & 7)
   // + 4 (l >> 4) + r, k = k0 + 128 wk + 16 j + (l & 15)
@@ -492,7 +502,8 @@ struct PPPlan {
 
 // rounds of 256-CU workgroup waves x per-workgroup MFMA time, plus the partial-sum traffic of the
 // epilogue (slabs: stored and re-read at ~5 TB/s; atomics ~1.3 TB/s)
-PPPlan plan_pp(int M, int N, int K, int split_req, int mode_req, int ncu, int min_split) {
+// gran: row granularity of a chunk (W4 runs stages in groups of four)
+PPPlan plan_pp(int M, int N, int K, int split_req, int mode_req, int ncu, int min_split, int gran) {
   PPPlan p;
   const int tiles_n = (N + wpp::TW - 1) / wpp::TW;
   p.tiles_k = (K + wpp::TW - 1) / wpp::TW;
@@ -501,7 +512,7 @@ PPPlan plan_pp(int M, int N, int K, int split_req, int mode_req, int ncu, int mi
   const int max_split = (M + wpp::BR - 1) / wpp::BR;
   auto eval = [&](int s) {
     int chunk = (M + s - 1) / s;
-    chunk = (chunk + wpp::BR - 1) / wpp::BR * wpp::BR;
+    chunk = (chunk + gran - 1) / gran * gran;
     const int ss = (M + chunk - 1) / chunk;
     const long long nwg = (long long)p.tiles * ss;
     const long long rounds = (nwg + ncu - 1) / ncu;
@@ -540,7 +551,7 @@ hipError_t plan_wgrad_pp(int lda, int ldb, int M, int N, int K, int split, int m
   // deterministic runs never use atomics
   // W4 keeps its accumulators in AGPRs through the slab epilogue only (a direct C epilogue made the
   // register allocator spill): always slabs, also for split 1
-  p = plan_pp(M, N, K, split, det || variant == 1 ? 0 : mode, device_cu_count(), 1);
+  p = plan_pp(M, N, K, split, det || variant == 1 ? 0 : mode, device_cu_count(), 1, variant == 1 ? 4 * wpp::BR : wpp::BR);
   if (variant == 1) p.mode = 0;  // (the plan picks the direct C epilogue, mode 1, for split 1)
   p.slabs = p.mode == 0 && (p.split > 1 || variant == 1);
   return hipSuccess;

@@ -7,7 +7,9 @@
 #   tests              pytest -m gpu (one process, per-test timeout)
 #   smoke              __graft_entry__.smoke()
 #   bench[:MB[:ARGS]]  bench.py --gpus 1 at micro-batch MB (default 128); ARGS: extra flags, ',' for ' '
-#   prof[:MB]          rocprofv3 kernel trace of a short bench run -> OUT/kernel_stats_mbMB.txt (per step)
+#   prof[:MB[:ARGS]]   rocprofv3 kernel trace of a short bench run -> OUT/kernel_stats_TAG.txt (per step;
+#                      TAG = $PROF_TAG or mbMB; ARGS: extra bench flags, ',' for ' ')
+#   tune[:MB[:ARGS]]   scripts/tune_gemms.sh (TunableOp pass over the bench's library GEMMs, AB=0)
 #   det[:ENV]          bench/determinism_probe.py (ENV e.g. LLMTRAIN_WGRAD_STREAM=0)
 #   detruns[:ENV]      3 whole deterministic runs of DET_STEPS (400) steps, compared step by step
 #   gloo2              bench.py --gpus 2 --backend gloo on the one GPU (rehearses the 2-rank path)
@@ -41,14 +43,15 @@ for step in "$@"; do
       mb=${arg%%:*}; mb=${mb:-128}; extra=""; [[ "$arg" == *:* ]] && extra=${arg#*:}
       run "bench_mb$mb" 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 --micro-batch "$mb" ${extra//,/ } ;;
     prof)
-      mb=${arg:-128}; d="$OUT/prof_mb$mb"; mkdir -p "$d"
-      run "prof_mb$mb" 600 rocprofv3 --kernel-trace --output-format rocpd -d "$d" -o run -- \
-        python3 bench.py --gpus 1 --steps 6 --warmup 3 --micro-batch "$mb"
+      mb=${arg%%:*}; mb=${mb:-128}; extra=""; [[ "$arg" == *:* ]] && extra=${arg#*:}
+      tag=${PROF_TAG:-mb$mb}; d="$OUT/prof_$tag"; mkdir -p "$d"
+      run "prof_$tag" 600 rocprofv3 --kernel-trace --output-format rocpd -d "$d" -o run -- \
+        python3 bench.py --gpus 1 --steps 6 --warmup 3 --micro-batch "$mb" ${extra//,/ }
       db=$(find "$d" -name "*.db" | head -1)
-      python3 scripts/rocpd_stats.py "$db" 3 40 > "$OUT/kernel_stats_mb$mb.txt" 2>&1 || true
-      python3 scripts/rocpd_timeline.py "$db" 3 > "$OUT/timeline_mb$mb.txt" 2>&1 || true
+      python3 scripts/rocpd_stats.py "$db" 3 40 > "$OUT/kernel_stats_$tag.txt" 2>&1 || true
+      python3 scripts/rocpd_timeline.py "$db" 3 > "$OUT/timeline_$tag.txt" 2>&1 || true
       rm -f "$db"
-      cat "$OUT/kernel_stats_mb$mb.txt" ;;
+      cat "$OUT/kernel_stats_$tag.txt" ;;
     det)
       name=det${arg:+_${arg//[^A-Za-z0-9]/_}}
       echo "== $name"
@@ -67,6 +70,9 @@ for step in "$@"; do
     ab) envs=${arg%%:*}; rest=""; [[ "$arg" == *:* ]] && rest=${arg#*:}
       IFS='|' read -r -a E <<< "$envs"
       run ab 1000 bash scripts/abn.sh "${E[@]}" -- ${rest//,/ } ;;
+    tune)
+      mb=${arg%%:*}; mb=${mb:-128}; extra=""; [[ "$arg" == *:* ]] && extra=${arg#*:}
+      run "tune_$mb" 1000 env MB="$mb" BENCH_ARGS="${extra//,/ }" AB=0 bash scripts/tune_gemms.sh ;;
     wpp) run "wpp_${arg%%,*}" 300 python -u bench/wgrad_pp.py ${arg//,/ } ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -40,7 +40,7 @@ def check() -> int:
     cases = [(4096, n, k, name) for model in ("gpt2-124m", "gpt2-xl") for name, (n, k) in SHAPES[model].items()]
     cases += [(1000, 2304, 768, "ragged M"), (3 * 32 + 5, 768, 768, "tiny M"), (2048, 50257, 768, "head")]
     for M, N, K, name in cases:
-        for mode, variant in ((-1, 0), (0, 0), (2, 0), (-1, 1)):
+        for mode in (-1, 0, 2):
             lda = 50304 if N == 50257 else N
             base = torch.randn(M, lda, device="cuda", dtype=torch.bfloat16)
             dy = base[:, :N]
@@ -48,14 +48,14 @@ def check() -> int:
             c0 = torch.randn(N, K, device="cuda")
             b0 = torch.randn(N, device="cuda")
             c, b = c0.clone(), b0.clone()
-            ops.wgrad_gemm_pp(dy, x, c, b, 0, mode, variant)
+            ops.wgrad_gemm_pp(dy, x, c, b, 0, mode)
             ref = c0 + dy.float().t() @ x.float()
             rb = b0 + dy.float().sum(0)
             err = ((c - ref).abs().max() / ref.abs().max()).item()
             berr = ((b - rb).abs().max() / rb.abs().max()).item()
             ok = err < 2e-5 and berr < 2e-5
             bad += not ok
-            print(json.dumps({"case": name, "M": M, "N": N, "K": K, "mode": mode, "variant": variant, "rel_err": err,
+            print(json.dumps({"case": name, "M": M, "N": N, "K": K, "mode": mode, "rel_err": err,
                               "bias_rel_err": berr, "ok": ok}), flush=True)
     # run-to-run bitwise (slab mode)
     dy = torch.randn(8192, 2304, device="cuda", dtype=torch.bfloat16)
@@ -82,8 +82,6 @@ def time_shapes(model: str, M: int, only: str = "") -> None:
         flops = 2.0 * M * N * K
         variants = {
             "pp_auto": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, -1),
-            "w4": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, -1, 1),
-            "w4_bias": lambda: ops.wgrad_gemm_pp(dy, x, acc, bias, 0, -1, 1),
             "pp_slab": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, 0),
             "pp_atomic": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, 2),
             "pp_slab_bias": lambda: ops.wgrad_gemm_pp(dy, x, acc, bias, 0, 0),
@@ -104,8 +102,7 @@ def one(gemm: str, variant: str, M: int, reps: int) -> None:
     dy = torch.randn(M, lda, device="cuda", dtype=torch.bfloat16)[:, :N]
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     acc = torch.zeros(N, K, device="cuda")
-    fn = {"pp": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, -1),
-          "w4": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, -1, 1)}[variant]
+    fn = {"pp": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, -1)}[variant]
     for _ in range(reps):
         fn()
     torch.cuda.synchronize()

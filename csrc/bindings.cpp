@@ -482,7 +482,7 @@ Tensor dropout_mask(int64_t n, double p, int64_t seed, const Tensor& like) {
 // ---- weight-gradient GEMM --------------------------------------------------------------------
 // dst[N, K] (fp32) += dy[M, N]^T x[M, K], and bias[N] += colsum(dy) when given (ping-pong kernel)
 void wgrad_gemm_pp(const Tensor& dy, const Tensor& x, Tensor c, const c10::optional<Tensor>& bias, int64_t split,
-                   int64_t mode, int64_t variant) {
+                   int64_t mode) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && c.is_cuda(), "wgrad_gemm_pp: GPU tensors required");
   check_dtype(dy, at::kBFloat16, "dy");
   check_dtype(x, at::kBFloat16, "x");
@@ -502,11 +502,11 @@ void wgrad_gemm_pp(const Tensor& dy, const Tensor& x, Tensor c, const c10::optio
   }
   at::hip::HIPGuardMasqueradingAsCUDA guard(c.device());
   const long wsf = llmt::wgrad_pp_ws_floats((int)dy.stride(0), (int)x.stride(0), (int)M, (int)N, (int)K, (int)split,
-                                            (int)mode, bptr != nullptr, (int)variant);
+                                            (int)mode, bptr != nullptr);
   Tensor ws = workspace(c, wsf);
   check_hip(llmt::launch_wgrad_pp(dy.data_ptr(), (int)dy.stride(0), x.data_ptr(), (int)x.stride(0),
                                   c.data_ptr<float>(), (int)c.stride(0), (int)M, (int)N, (int)K, (int)split, (int)mode,
-                                  wsf > 0 ? ws.data_ptr<float>() : nullptr, bptr, cur_stream(), (int)variant),
+                                  wsf > 0 ? ws.data_ptr<float>() : nullptr, bptr, cur_stream()),
             "wgrad_gemm_pp");
 }
 
@@ -690,8 +690,7 @@ TORCH_LIBRARY(llmtrain_hip, m) {
   m.def("set_deterministic(bool on) -> ()", &set_deterministic);  // catch-all: no tensor arguments
   m.def("get_deterministic() -> bool", &get_deterministic);
   m.def("set_dropout_seed_offset(Tensor? word) -> ()", &set_dropout_seed_offset);
-  m.def("wgrad_gemm_pp(Tensor dy, Tensor x, Tensor(a!) c, Tensor(b!)? bias=None, int split=0, int mode=-1,"
-        " int variant=0) -> ()");
+  m.def("wgrad_gemm_pp(Tensor dy, Tensor x, Tensor(a!) c, Tensor(b!)? bias=None, int split=0, int mode=-1) -> ()");
   m.def("gemm_fused(Tensor a, Tensor b, bool b_kn, int epilogue, Tensor? bias=None, Tensor? u=None,"
         " Tensor(a!)? dbias=None, int seq_len=0) -> (Tensor, Tensor?)");
   m.def("sumsq(Tensor x) -> Tensor");

@@ -261,195 +261,9 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_pp_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// Four accumulate-in-place MFMAs on accumulators pinned to AGPRs ("+a": the 256 accumulators fill
-// the AGPR file exactly, and the builtin let the register allocator stage them through VGPRs, with
-// hundreds of v_accvgpr moves and spills per stage).  Inside the statement nothing is padded: the
-// leading s_nop 1 covers a VALU-written operand, and consecutive MFMAs on different accumulators
-// need no wait states (an accumulator's next reader is the next stage's MFMA of the same slot).
-__device__ __forceinline__ void mfma4(f32x4v& c0, f32x4v& c1, f32x4v& c2, f32x4v& c3, const bf16x8& a,
-                                      const bf16x8& b0, const bf16x8& b1, const bf16x8& b2, const bf16x8& b3) {
-  asm volatile(
-      "s_nop 1\n\t"
-      "v_mfma_f32_16x16x32_bf16 %0, %4, %5, %0\n\t"
-      "v_mfma_f32_16x16x32_bf16 %1, %4, %6, %1\n\t"
-      "v_mfma_f32_16x16x32_bf16 %2, %4, %7, %2\n\t"
-      "v_mfma_f32_16x16x32_bf16 %3, %4, %8, %3"
-      : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3)
-      : "v"(a), "v"(b0), "v"(b1), "v"(b2), "v"(b3));
-}
-
-// W4: the same 256 x 256 tile with ONE wave per SIMD (256-thread workgroups), each wave owning a
-// 128 (n) x 128 (k) quarter = 8 x 8 v_mfma_f32_16x16x32_bf16 accumulators (256 AGPRs).  Per 32-row
-// stage a CU reads 64 KiB of fragments (8 A + 8 B per wave) for 4 x 64 MFMAs, against 96 KiB for
-// the 8-wave 128 x 64 ping-pong above: 1/3 fewer LDS bytes per FLOP, the LDS budget that kept that
-// schedule at ~1.1 PF (docs/round4.md section 1).  With no partner wave to cover its loads, each
-// wave software-pipelines itself: stage s's 64 MFMAs run from registers while the same wave reads
-// stage s+1's fragments (A fragments re-read in place after their last use, B double-buffered),
-// writes stage s+2 into its LDS slot and loads stage s+4 (two register sets: a load has two stages
-// to land), the four kinds of work interleaved in 16 pinned groups of 4 MFMAs (sched_barrier), one
-// barrier per stage.  Four 32 KiB slots: a slot is rewritten two stages after its fragments were
-// read, so the barrier only waits for this wave's writes (counted lgkmcnt) and the fragment reads
-// of the stage's last groups stay in flight across it (a 2-slot ring exposed them at every stage).
-__global__ __launch_bounds__(256, 1) void wgrad_w4_kernel(
-    const bf16_raw* __restrict__ A, int lda, const bf16_raw* __restrict__ B, int ldb, float* __restrict__ C,
-    int ldc, int M, int N, int K, int tiles, int tiles_k, int m_chunk, int split, int nwg, float* __restrict__ slab,
-    float* __restrict__ bias_slab) {
-  __shared__ __attribute__((aligned(16))) bf16_raw smem[4 * SLOT / 2];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wn = wave >> 1, wk = wave & 1;
-
-  const int w = xcd_remap(blockIdx.x, nwg);
-  const int chunk = w / tiles, tile = w - chunk * tiles;
-  const int tile_n = tile / tiles_k, tile_k = tile - tile_n * tiles_k;
-  const int n0 = tile_n * TW, k0 = tile_k * TW;
-  const int m_begin = chunk * m_chunk;
-  const int rows = min(M - m_begin, m_chunk);
-  if (rows <= 0) return;
-  const int nst = (rows + BR - 1) / BR;
-  const bool want_bias = bias_slab != nullptr && tile_k == 0;
-
-  // fills: wave w copies image rows 8w .. 8w+7 of A and of B, four 1-KiB pieces each (two rows per
-  // piece); lane l lands at 16-byte chunk (l & 31) of its row and holds the source chunk whose
-  // 32-byte segment is that one XOR f(row)
-  int voa[4], vob[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int row = 8 * wave + 2 * j + (lane >> 5);
-    const int c = lane & 31;
-    const int csrc = ((((c >> 1) ^ swz_f(row))) << 1) | (c & 1);
-    voa[j] = (row * lda + n0 + 8 * csrc) * 2;
-    vob[j] = (row * ldb + k0 + 8 * csrc) * 2;
-  }
-  const unsigned lds = (unsigned)(unsigned long)(lds_void*)smem;
-
-  // fragment addresses: A fragment i = logical segment 8 wn + ((i + 4 wk) & 7) (the rotation puts
-  // the 4 fragments whose bias column sums this wave forms at i = 0..3), B fragment j = 8 wk + j
-  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-  const int fl = q | ((g & 1) << 2);
-  const unsigned rowb = (unsigned)((8 * g + q) * ROWB + 8 * p);
-  unsigned ao[8], bo[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) ao[i] = rowb + ((8 * wn + (((i + 4 * wk) & 7) ^ fl)) << 5);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bo[j] = IMG + rowb + ((8 * wk + (j ^ fl)) << 5);
-
-  f32x4v acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
-  f32x4v bacc[4] = {0.f, 0.f, 0.f, 0.f};
-  const bf16x8 ones = __builtin_bit_cast(bf16x8, (short8v){0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
-
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
-  u32x4 R0[8], R1[8];  // staged stages (even, odd): A pieces 0-3, B pieces 4-7
-  // unconditional loads: a stage past the chunk has a zero-record descriptor and loads zeros
-  auto load_piece = [&](u32x4 (&R)[8], int st, int j) {
-    const int r0 = st * BR, nr = max(0, min(BR, rows - r0));
-    if (j < 4) {
-      const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(A + (long)(m_begin + r0) * lda, nr * lda * 2);
-      R[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, voa[j], 0, 0));
-    } else {
-      const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(B + (long)(m_begin + r0) * ldb, nr * ldb * 2);
-      R[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, vob[j - 4], 0, 0));
-    }
-  };
-  auto write_piece = [&](const u32x4 (&R)[8], int slot, int j) {
-    const unsigned a = lds + slot * SLOT + (j < 4 ? 0 : IMG) + wave * 4096 + (j & 3) * 1024 + 16 * lane;
-    *(lds_u32x4*)(size_t)a = R[j];
-  };
-  auto read_frag = [&](int slot, int f) -> bf16x8 {
-    return tr_read(lds + slot * SLOT + (f < 8 ? ao[f] : bo[f - 8]));
-  };
-
-  // prologue: stages 0 and 1 in slots 0 and 1, stages 2 and 3 loading, stage 0's fragments in
-  // registers
-  bf16x8 fa[8], fb[8], gb[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) load_piece(R0, 0, j);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) load_piece(R1, 1, j);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) write_piece(R0, 0, j);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) write_piece(R1, 1, j);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) load_piece(R0, 2, j);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) load_piece(R1, 3, j);
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#pragma unroll
-  for (int f = 0; f < 8; ++f) fa[f] = read_frag(0, f);
-#pragma unroll
-  for (int f = 0; f < 8; ++f) fb[f] = read_frag(0, 8 + f);
-
-  // one stage: MFMAs on (fa, cb) = stage st, A-fragment-major, so A fragment i is dead after
-  // groups 2i and 2i+1 and its successor of stage st+1 is read into the same registers (single
-  // buffer); the B fragments are used by every group and double-buffered (cb -> nb).  Stage st+1
-  // is in slot (st+1) % 4; stage st+2 (in R, loaded two stages ago) goes into slot (st+2) % 4, whose
-  // last reads (stage st-2's fragments) ended two barriers ago; stage st+4 is loaded into R.
-  auto stage = [&](int st, int rs, int ws, u32x4 (&R)[8], bf16x8 (&cb)[8], bf16x8 (&nb)[8]) {
-#pragma unroll
-    for (int grp = 0; grp < 16; ++grp) {
-      const int i = grp >> 1, j0 = 4 * (grp & 1);
-      mfma4(acc[i][j0], acc[i][j0 + 1], acc[i][j0 + 2], acc[i][j0 + 3], fa[i], cb[j0], cb[j0 + 1], cb[j0 + 2],
-            cb[j0 + 3]);
-      if (grp < 8 && (grp & 1) == 0 && want_bias)  // column sums of A fragments 0-3 (this wave's share)
-        asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(bacc[i]) : "v"(fa[i]), "v"(ones));
-      if (grp & 1) fa[i] = read_frag(rs, i);  // A fragment i of stage st+1 (its last use was above)
-      else nb[grp >> 1] = read_frag(rs, 8 + (grp >> 1));
-      if (grp >= 8 && grp < 12) {  // stage st+2 into its slot
-        write_piece(R, ws, 2 * (grp - 8));
-        write_piece(R, ws, 2 * (grp - 8) + 1);
-      }
-      if (grp >= 12) {  // stage st+4 into the registers just written out
-        load_piece(R, st + 4, 2 * (grp - 12));
-        load_piece(R, st + 4, 2 * (grp - 12) + 1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // this wave's writes of stage st+2 have landed (the 8 fragment reads of groups 12-15, issued
-    // after them, may still be in flight: the slot they read is rewritten two stages later), then
-    // the barrier
-    asm volatile("s_waitcnt lgkmcnt(8)\n\ts_barrier" ::: "memory");
-  };
-  // groups of four unconditional stages (slots, register sets and B buffers compile-time in each);
-  // the stage count is padded with stages of zeros to a multiple of 4
-  for (int s0 = 0; s0 < nst; s0 += 4) {
-    stage(s0, 1, 2, R0, fb, gb);
-    stage(s0 + 1, 2, 3, R1, gb, fb);
-    stage(s0 + 2, 3, 0, R0, fb, gb);
-    stage(s0 + 3, 0, 1, R1, gb, fb);
-  }
-  asm volatile("s_nop 15" ::: "memory");  // the last MFMAs' results settle before compiler code reads them
-  // the loads and fragment reads past the last stage land before the epilogue (and the exit)
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-
-  // ---- epilogue.  Accumulator (i, j) register r of lane l: n = n0 + 128 wn + 16 ((i + 4 wk) & 7)
-  // + 4 (l >> 4) + r, k = k0 + 128 wk + 16 j + (l & 15)
-  if (want_bias) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int r = lane & 3;
-      const float v = r == 0 ? bacc[t][0] : r == 1 ? bacc[t][1] : r == 2 ? bacc[t][2] : bacc[t][3];
-      const int n = n0 + 128 * wn + 16 * (4 * wk + t) + 4 * g + r;
-      if ((lane & 15) < 4 && n < N) bias_slab[(long)chunk * N + n] = v;
-    }
-  }
-  // accumulators to this (tile, chunk)'s slab: [wave][accumulator][lane][4], 16-byte stores
-  float* sl = slab + ((long)(tile * split + chunk) * 4 + wave) * (64 * 64 * 4);
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) *(f32x4v*)(sl + ((i * 8 + j) * 64 + lane) * 4) = acc[i][j];
-}
-
 // One finishing launch per GEMM: threads [0, total) add the split slabs of each tile to C in chunk
 // order (bitwise reproducible; one thread per (tile, wave, accumulator, lane): a 16-byte load per
 // slab, 4 output rows), threads [total, total + nbias) add the bias partial rows in chunk order.
-template <bool W4>
 __global__ __launch_bounds__(256) void wgrad_finish_kernel(const float* __restrict__ slab, int split,
                                                           float* __restrict__ C, int ldc, int N, int K, int tiles_k,
                                                           long total, const float* __restrict__ bias_parts,
@@ -463,26 +277,18 @@ __global__ __launch_bounds__(256) void wgrad_finish_kernel(const float* __restri
     bias[n] += s;
     return;
   }
-  // slab layout per tile: [wave][accumulator][lane][4]; 8 waves x 32 (ping-pong) or 4 x 64 (W4)
-  constexpr int WAVES = W4 ? 4 : 8, NA = W4 ? 64 : NACC;
   const int lane = (int)(t & 63);
   const long u = t >> 6;               // (tile, wave, acc)
-  const int a = (int)(u % NA);
-  const long v = u / NA;               // (tile, wave)
-  const int wave = (int)(v % WAVES);
-  const long tile = v / WAVES;
+  const int a = (int)(u % NACC);
+  const long v = u / NACC;             // (tile, wave)
+  const int wave = (int)(v & 7);
+  const long tile = v >> 3;
+  const int i = a / FB, j = a - i * FB;
+  const int wn = wave >> 2, wk = wave & 3;
   const int tile_n = (int)(tile / tiles_k), tile_k = (int)(tile - (long)tile_n * tiles_k);
-  int k, nb;
-  if (W4) {
-    const int i = a >> 3, j = a & 7, wn = wave >> 1, wk = wave & 1;
-    k = tile_k * TW + 128 * wk + 16 * j + (lane & 15);
-    nb = tile_n * TW + 128 * wn + 16 * ((i + 4 * wk) & 7) + 4 * (lane >> 4);
-  } else {
-    const int i = a / FB, j = a - i * FB, wn = wave >> 2, wk = wave & 3;
-    k = tile_k * TW + 64 * wk + 16 * j + (lane & 15);
-    nb = tile_n * TW + 128 * wn + 16 * ((i + 2 * wk) & 7) + 4 * (lane >> 4);
-  }
-  const float* src = slab + (tile * split * WAVES + wave) * (long)(NA * 64 * 4) + (a * 64 + lane) * 4;
+  const int k = tile_k * TW + 64 * wk + 16 * j + (lane & 15);
+  const int nb = tile_n * TW + 128 * wn + 16 * ((i + 2 * wk) & 7) + 4 * (lane >> 4);
+  const float* src = slab + (tile * split * 8 + wave) * (long)(NACC * 64 * 4) + (a * 64 + lane) * 4;
   f32x4v sum = *(const f32x4v*)src;
   for (int s = 1; s < split; ++s) sum += *(const f32x4v*)(src + (long)s * SLAB_FLOATS);
   if (k >= K) return;
@@ -502,8 +308,7 @@ struct PPPlan {
 
 // rounds of 256-CU workgroup waves x per-workgroup MFMA time, plus the partial-sum traffic of the
 // epilogue (slabs: stored and re-read at ~5 TB/s; atomics ~1.3 TB/s)
-// gran: row granularity of a chunk (W4 runs stages in groups of four)
-PPPlan plan_pp(int M, int N, int K, int split_req, int mode_req, int ncu, int min_split, int gran) {
+PPPlan plan_pp(int M, int N, int K, int split_req, int mode_req, int ncu, int min_split) {
   PPPlan p;
   const int tiles_n = (N + wpp::TW - 1) / wpp::TW;
   p.tiles_k = (K + wpp::TW - 1) / wpp::TW;
@@ -512,7 +317,7 @@ PPPlan plan_pp(int M, int N, int K, int split_req, int mode_req, int ncu, int mi
   const int max_split = (M + wpp::BR - 1) / wpp::BR;
   auto eval = [&](int s) {
     int chunk = (M + s - 1) / s;
-    chunk = (chunk + gran - 1) / gran * gran;
+    chunk = (chunk + wpp::BR - 1) / wpp::BR * wpp::BR;
     const int ss = (M + chunk - 1) / chunk;
     const long long nwg = (long long)p.tiles * ss;
     const long long rounds = (nwg + ncu - 1) / ncu;
@@ -544,34 +349,31 @@ PPPlan plan_pp(int M, int N, int K, int split_req, int mode_req, int ncu, int mi
   return p;
 }
 
-hipError_t plan_wgrad_pp(int lda, int ldb, int M, int N, int K, int split, int mode, bool det, int variant, PPPlan& p) {
+hipError_t plan_wgrad_pp(int lda, int ldb, int M, int N, int K, int split, int mode, bool det, PPPlan& p) {
   if (lda % 8 || ldb % 8 || K % 8 || lda < N) return hipErrorInvalidValue;
   // one stage of either operand must stay below the 32-bit buffer range
   if ((long long)wpp::BR * std::max(lda, ldb) * 2 >= (1LL << 31)) return hipErrorInvalidValue;
   // deterministic runs never use atomics
-  // W4 keeps its accumulators in AGPRs through the slab epilogue only (a direct C epilogue made the
-  // register allocator spill): always slabs, also for split 1
-  p = plan_pp(M, N, K, split, det || variant == 1 ? 0 : mode, device_cu_count(), 1, variant == 1 ? 4 * wpp::BR : wpp::BR);
-  if (variant == 1) p.mode = 0;  // (the plan picks the direct C epilogue, mode 1, for split 1)
-  p.slabs = p.mode == 0 && (p.split > 1 || variant == 1);
+  p = plan_pp(M, N, K, split, det ? 0 : mode, device_cu_count(), 1);
+  p.slabs = p.mode == 0 && p.split > 1;
   return hipSuccess;
 }
 }  // namespace
 
-long wgrad_pp_ws_floats(int lda, int ldb, int M, int N, int K, int split, int mode, bool bias, int variant) {
+long wgrad_pp_ws_floats(int lda, int ldb, int M, int N, int K, int split, int mode, bool bias) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   PPPlan p;
-  if (plan_wgrad_pp(lda, ldb, M, N, K, split, mode, deterministic(), variant, p) != hipSuccess) return 0;
+  if (plan_wgrad_pp(lda, ldb, M, N, K, split, mode, deterministic(), p) != hipSuccess) return 0;
   long f = p.slabs ? (long)p.tiles * p.split * wpp::SLAB_FLOATS : 0;
   if (bias && !(p.mode == 2 && p.split > 1)) f += (long)p.split * N;
   return f;
 }
 
 hipError_t launch_wgrad_pp(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N, int K,
-                           int split, int mode, float* ws, float* bias, hipStream_t stream, int variant) {
+                           int split, int mode, float* ws, float* bias, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return hipSuccess;
   PPPlan p;
-  const hipError_t e = plan_wgrad_pp(lda, ldb, M, N, K, split, mode, deterministic(), variant, p);
+  const hipError_t e = plan_wgrad_pp(lda, ldb, M, N, K, split, mode, deterministic(), p);
   if (e != hipSuccess) return e;
   const int nwg = p.tiles * p.split;
   const bool slabs = p.slabs;
@@ -581,29 +383,19 @@ hipError_t launch_wgrad_pp(const void* dy, int lda, const void* x, int ldb, floa
       bias == nullptr ? nullptr : atomic ? bias : ws + (slabs ? (long)p.tiles * p.split * wpp::SLAB_FLOATS : 0);
   if ((slabs || (bias != nullptr && !atomic)) && ws == nullptr) return hipErrorInvalidValue;
   const int m = slabs ? 0 : (p.split == 1 ? 1 : 2);
-#define LLMT_WPP_LAUNCH(KERNEL, THREADS)                                                                          \
-  hipLaunchKernelGGL(KERNEL, dim3(nwg), dim3(THREADS), 0, stream, (const bf16_raw*)dy, lda, (const bf16_raw*)x, ldb, \
-                     c, ldc, M, N, K, p.tiles, p.tiles_k, p.m_chunk, p.split, nwg, slab, bias_parts)
-  if (variant == 1) {
-    if (!slabs || slab == nullptr) return hipErrorInvalidValue;  // W4 has no other epilogue
-    LLMT_WPP_LAUNCH(wpp::wgrad_w4_kernel, 256);
-  } else {
-    if (m == 0) LLMT_WPP_LAUNCH(wpp::wgrad_pp_kernel<0>, wpp::kThreads);
-    else if (m == 1) LLMT_WPP_LAUNCH(wpp::wgrad_pp_kernel<1>, wpp::kThreads);
-    else LLMT_WPP_LAUNCH(wpp::wgrad_pp_kernel<2>, wpp::kThreads);
-  }
+#define LLMT_WPP_LAUNCH(MD)                                                                                    \
+  hipLaunchKernelGGL(wpp::wgrad_pp_kernel<MD>, dim3(nwg), dim3(wpp::kThreads), 0, stream, (const bf16_raw*)dy, lda,  \
+                     (const bf16_raw*)x, ldb, c, ldc, M, N, K, p.tiles, p.tiles_k, p.m_chunk, p.split, nwg, slab,      \
+                     bias_parts)
+  if (m == 0) LLMT_WPP_LAUNCH(0);
+  else if (m == 1) LLMT_WPP_LAUNCH(1);
+  else LLMT_WPP_LAUNCH(2);
 #undef LLMT_WPP_LAUNCH
   const long total = slabs ? (long)p.tiles * wpp::SLAB_FLOATS / 4 : 0;
   const int nbias = bias != nullptr && !atomic ? N : 0;
-  if (total + nbias > 0) {
-    const dim3 grid((unsigned)((total + nbias + 255) / 256));
-    if (variant == 1)
-      hipLaunchKernelGGL(wpp::wgrad_finish_kernel<true>, grid, dim3(256), 0, stream, slab, p.split, c, ldc, N, K,
-                         p.tiles_k, total, bias_parts, bias, nbias);
-    else
-      hipLaunchKernelGGL(wpp::wgrad_finish_kernel<false>, grid, dim3(256), 0, stream, slab, p.split, c, ldc, N, K,
-                         p.tiles_k, total, bias_parts, bias, nbias);
-  }
+  if (total + nbias > 0)
+    hipLaunchKernelGGL(wpp::wgrad_finish_kernel, dim3((unsigned)((total + nbias + 255) / 256)), dim3(256), 0, stream,
+                       slab, p.split, c, ldc, N, K, p.tiles_k, total, bias_parts, bias, nbias);
   return hipGetLastError();
 }
 

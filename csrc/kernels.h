@@ -145,10 +145,9 @@ hipError_t launch_sumsq(const float* x, long long n, float* partials, float* out
 // Ping-pong weight-gradient GEMM (gemm_wgrad_pp.hip): C[N,K] += dy^T x and, with `bias`,
 // bias[N] += colsum(dy).  `ws` holds wgrad_pp_ws_floats(...) floats (split slabs + bias parts).
 // mode: -1 auto, 0 slabs + fixed-order reduce, 2 fp32 atomics (ignored in deterministic mode).
-long wgrad_pp_ws_floats(int lda, int ldb, int M, int N, int K, int split, int mode, bool bias, int variant = 0);
-// variant: 0 = the 8-wave ping-pong kernel, 1 = W4 (4 waves x 128 x 128, one wave per SIMD)
+long wgrad_pp_ws_floats(int lda, int ldb, int M, int N, int K, int split, int mode, bool bias);
 hipError_t launch_wgrad_pp(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N, int K,
-                           int split, int mode, float* ws, float* bias, hipStream_t stream, int variant = 0);
+                           int split, int mode, float* ws, float* bias, hipStream_t stream);
 // ---- forward / data-gradient GEMM with fused epilogues (bf16 in, fp32 accumulate, bf16 out)
 // C[M, N] = epi(A[M, K] . op(B)); B is [N, ldb] (K contiguous, b_kn = false) or [K, ldb]
 // (N contiguous, b_kn = true).  epilogue 0: C = acc + bias (bias optional);

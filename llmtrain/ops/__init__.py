@@ -519,19 +519,13 @@ def linear_dx_attn(dy, w, att, seqlen: int, v_bias_grad=None, head_dim: int = 64
     return _lib_mm(dy, w, op="attention out-projection dX"), None
 
 
-# weight-gradient kernel of csrc/gemm_wgrad_pp.hip: "pp" = 8 waves x 128 x 64 (ping-pong), "w4" = 4
-# waves x 128 x 128 (one wave per SIMD, AGPR-pinned accumulators)
-WGRAD_KERNEL = os.environ.get("LLMTRAIN_WGRAD_KERNEL", "pp")
-_WGRAD_VARIANT = {"pp": 0, "w4": 1}[WGRAD_KERNEL]
-
-
 def wgrad_accum(dst, dy, x, *, bias=None) -> None:
     """``dst (fp32 [N, K]) += dy[M, N]^T @ x[M, K]`` and, with ``bias`` (fp32 ``[N]``),
     ``bias += colsum(dy)`` — the weight and bias gradients of an nn.Linear whose output gradient
     is ``dy`` (``dy`` may be a column slice with a larger row stride).  GPU: the split-K MFMA GEMM
     of csrc/gemm_wgrad_pp.hip with the bias column sums fused."""
     if _on_gpu(dst):
-        hip_ops().wgrad_gemm_pp(dy, x, dst, bias, 0, -1, _WGRAD_VARIANT)
+        hip_ops().wgrad_gemm_pp(dy, x, dst, bias, 0, -1)
         return
     dst.addmm_(dy.t().float(), x.float())
     if bias is not None:

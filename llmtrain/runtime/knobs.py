@@ -23,11 +23,6 @@ KNOBS: dict[str, tuple[str, str]] = {
         "1: weight-gradient GEMMs on a side stream beside the main stream (one stream measured faster "
         "since round 4, profiles/r4/ab_side_stream_vs_one_stream_mb*.txt)",
     ),
-    "LLMTRAIN_WGRAD_KERNEL": (
-        "pp",
-        "weight-gradient kernel: `pp` (8 waves x 128 x 64 per wave, ping-pong) or `w4` (4 waves x 128 x 128, "
-        "one wave per SIMD)",
-    ),
     "LLMTRAIN_FUSED_GEMM": (
         "1",
         "0: plain hipBLASLt GEMMs with separate GELU / attention-delta passes instead of the fused-epilogue "

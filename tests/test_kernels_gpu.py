@@ -239,17 +239,16 @@ def test_layernorm_bwd_deferred_params_batched(gpu_device, M, d):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("mode", [-1, 0, 2])
 @pytest.mark.parametrize("M,N,K,lda", [(4096, 768, 768, 768), (2048, 2304, 768, 2304), (1000, 200, 72, 200),
                                         (3000, 1000, 768, 1024), (2080, 1600, 4800, 1600),
                                         (1500, 1001, 768, 1024), (101, 768, 768, 768),
                                         (2048, 50257, 768, 50304)])  # the LM head's padded logits
-def test_wgrad_gemm_pp(gpu_device, M, N, K, lda, mode, variant):
-    """Weight-gradient GEMM (csrc/gemm_wgrad_pp.hip; variant 0 = the 8-wave ping-pong kernel, 1 = W4):
-    dst += dY^T X and bias += colsum(dY) against fp32, for the auto plan, the slab (deterministic)
-    and the atomic epilogue (W4: slabs always), ragged M/N/K, a column-slice dY (row stride lda > N),
-    a single-stage chunk and an odd stage count (the zero-padded last stage)."""
+def test_wgrad_gemm_pp(gpu_device, M, N, K, lda, mode):
+    """Ping-pong weight-gradient GEMM (csrc/gemm_wgrad_pp.hip): dst += dY^T X and bias += colsum(dY)
+    against fp32, for the auto plan, the slab (deterministic) and the atomic epilogue, ragged M/N/K,
+    a column-slice dY (row stride lda > N), a single-stage chunk and an odd stage count (the
+    zero-padded last stage)."""
     g = torch.Generator(device="cpu").manual_seed(M + N + K + mode)
     dy = torch.randn(M, lda, generator=g).to(gpu_device, torch.bfloat16)[:, :N]
     x = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)
@@ -257,17 +256,16 @@ def test_wgrad_gemm_pp(gpu_device, M, N, K, lda, mode, variant):
     b = torch.randn(N, generator=g).to(gpu_device)
     want = c + dy.float().t() @ x.float()
     want_b = b + dy.float().sum(0)
-    hip().wgrad_gemm_pp(dy, x, c, b, 0, mode, variant)
+    hip().wgrad_gemm_pp(dy, x, c, b, 0, mode)
     _close(c, want, 2e-5 * want.abs().max().item(), 1e-4, "wgrad_pp")
     _close(b, want_b, 2e-5 * want_b.abs().max().item(), 1e-4, "wgrad_pp bias")
     # an explicit split and no bias
     c2 = torch.zeros(N, K, device=gpu_device)
-    hip().wgrad_gemm_pp(dy, x, c2, None, 3, mode, variant)
+    hip().wgrad_gemm_pp(dy, x, c2, None, 3, mode)
     _close(c2, dy.float().t() @ x.float(), 2e-5 * want.abs().max().item(), 1e-4, "wgrad_pp split=3")
 
 
-@pytest.mark.parametrize("variant", [0, 1])
-def test_wgrad_gemm_pp_slabs_bitwise(gpu_device, variant):
+def test_wgrad_gemm_pp_slabs_bitwise(gpu_device):
     """The slab epilogue reduces the split partials in a fixed order: repeated launches are equal
     bit for bit (the deterministic mode needs no separate path)."""
     g = torch.Generator(device="cpu").manual_seed(5)
@@ -277,7 +275,7 @@ def test_wgrad_gemm_pp_slabs_bitwise(gpu_device, variant):
     for _ in range(3):
         c = torch.zeros(2304, 768, device=gpu_device)
         b = torch.zeros(2304, device=gpu_device)
-        hip().wgrad_gemm_pp(dy, x, c, b, 0, 0, variant)
+        hip().wgrad_gemm_pp(dy, x, c, b, 0, 0)
         outs.append((c, b))
     for c, b in outs[1:]:
         assert torch.equal(c, outs[0][0]) and torch.equal(b, outs[0][1])

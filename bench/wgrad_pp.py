@@ -2,6 +2,8 @@
 
     python bench/wgrad_pp.py check            # numerics vs fp32 (every shape, bias, strided dy)
     python bench/wgrad_pp.py time [--tokens M] [--model gpt2-124m|gpt2-xl|head]
+    python bench/wgrad_pp.py sweep [--tokens M] [--model ...] [--splits 1,2,4] [--mode 0]
+                                              # fixed split counts (the planner's choice as split 0)
 
 Each timing line: kernel, shape, ms (median of 20), TFLOP/s on the 2*M*N*K GEMM FLOPs.
 """
@@ -73,6 +75,7 @@ def check() -> int:
 
 def time_shapes(model: str, M: int, only: str = "") -> None:
     ops = _ops()
+    _warm()
     for name, (N, K) in SHAPES[model].items():
         lda = 50304 if N == 50257 else N
         dy = torch.randn(M, lda, device="cuda", dtype=torch.bfloat16)[:, :N]
@@ -94,6 +97,35 @@ def time_shapes(model: str, M: int, only: str = "") -> None:
                               "TFLOPs": round(flops / ms / 1e9, 1)}), flush=True)
 
 
+def _warm(seconds: float = 1.0) -> None:
+    """Hold the chip busy before the first timing (the first shape otherwise times at ramping clocks)."""
+    import time
+
+    a = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+    t0 = time.time()
+    while time.time() - t0 < seconds:
+        for _ in range(10):
+            a @ a
+        torch.cuda.synchronize()
+
+
+def sweep(model: str, M: int, splits: str, mode: int) -> None:
+    """Time each shape at fixed split counts (0 = the planner's choice): where the row-chunk
+    quantisation and the slab traffic of the split epilogue cost."""
+    ops = _ops()
+    _warm()
+    for name, (N, K) in SHAPES[model].items():
+        lda = 50304 if N == 50257 else N
+        dy = torch.randn(M, lda, device="cuda", dtype=torch.bfloat16)[:, :N]
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        acc = torch.zeros(N, K, device="cuda")
+        flops = 2.0 * M * N * K
+        for s in (int(v) for v in splits.replace("+", ",").split(",")):
+            ms = timeit(lambda: ops.wgrad_gemm_pp(dy, x, acc, None, s, mode))
+            print(json.dumps({"model": model, "M": M, "gemm": name, "split": s, "mode": mode, "ms": round(ms, 4),
+                              "TFLOPs": round(flops / ms / 1e9, 1)}), flush=True)
+
+
 def one(gemm: str, variant: str, M: int, reps: int) -> None:
     """Run one shape / kernel ``reps`` times (a target for rocprofv3 counter passes)."""
     ops = _ops()
@@ -110,16 +142,22 @@ def one(gemm: str, variant: str, M: int, reps: int) -> None:
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["check", "time", "one"])
+    ap.add_argument("what", choices=["check", "time", "one", "sweep"])
     ap.add_argument("--gemm", default="qkv")
     ap.add_argument("--variant", default="pp")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default="", help="comma-separated variant labels (time)")
     ap.add_argument("--tokens", type=int, default=131072)
     ap.add_argument("--model", default="gpt2-124m", choices=sorted(SHAPES))
+    ap.add_argument("--splits", default="0,1,2,3,4,5,6,8")
+    ap.add_argument("--mode", type=int, default=0,
+                    help="sweep: 0 slabs + finishing launch, 2 atomics, -1 auto")
     args = ap.parse_args()
     if args.what == "check":
         return check()
+    if args.what == "sweep":
+        sweep(args.model, args.tokens, args.splits, args.mode)
+        return 0
     if args.what == "one":
         one(args.gemm, args.variant, args.tokens, args.reps)
         return 0

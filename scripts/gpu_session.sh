@@ -4,7 +4,7 @@
 #
 #   bash scripts/gpu_session.sh [-o OUTDIR] STEP [STEP ...]
 #
-#   tests              pytest -m gpu (one process, per-test timeout)
+#   tests[:EXPR]       pytest -m gpu (one process, per-test timeout; EXPR: pytest -k expression)
 #   smoke              __graft_entry__.smoke()
 #   bench[:MB[:ARGS]]  bench.py --gpus 1 at micro-batch MB (default 128); ARGS: extra flags, ',' for ' '
 #   prof[:MB[:ARGS]]   rocprofv3 kernel trace of a short bench run -> OUT/kernel_stats_TAG.txt (per step;
@@ -25,8 +25,10 @@ OUT=gpurun_out/session
 if [ "${1:-}" = "-o" ]; then OUT=$2; shift 2; fi
 mkdir -p "$OUT"
 
-run() {  # run NAME LIMIT CMD... : stdout/stderr to OUT/NAME.log, tail shown, exit on failure
+run() {  # run NAME LIMIT CMD... : stdout/stderr to OUT/NAME.log (NAME_2, _3.. when repeated), tail shown, exit on failure
   local name=$1 limit=$2; shift 2
+  local n=2 base=$name
+  while [ -e "$OUT/$name.log" ]; do name=${base}_$n; n=$((n + 1)); done
   echo "== $name: $*"
   timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
@@ -37,7 +39,11 @@ run() {  # run NAME LIMIT CMD... : stdout/stderr to OUT/NAME.log, tail shown, ex
 for step in "$@"; do
   kind=${step%%:*}; arg=""; [ "$kind" != "$step" ] && arg=${step#*:}
   case $kind in
-    tests) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    tests) if [ -n "$arg" ]; then
+        run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$arg"
+      else
+        run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+      fi ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)
       mb=${arg%%:*}; mb=${mb:-128}; extra=""; [[ "$arg" == *:* ]] && extra=${arg#*:}

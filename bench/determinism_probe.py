@@ -40,6 +40,9 @@ def main() -> int:
     ap.add_argument("--model", default="gpt2-124m")
     ap.add_argument("--dropout", type=float, default=0.0)
     ap.add_argument("--runs", type=int, default=0, help="compare N whole runs step by step instead")
+    ap.add_argument("--pollute-gib", type=float, default=0.0,
+                    help="--runs: before each run, fill this much freed device memory with a different "
+                         "random pattern (a kernel that reads memory it never wrote shows up as a divergence)")
     args = ap.parse_args()
 
     import importlib.util
@@ -67,35 +70,38 @@ def main() -> int:
     stream = trainer.batch_stream()
     bad_total = 0
     t0 = time.perf_counter()
-    for step in range(1, args.steps + 1):
-        batch = _to_device(stream.next(), trainer.device)
-        ref_grad = ref_loss = None
-        for rep in range(args.reps):
-            trainer.optimizer.zero_grad()
-            torch.manual_seed(1000 + step)  # the same dropout draw in every repetition
-            with trainer._policy.autocast():
-                loss, _ = trainer._adapter.compute_loss(trainer.model, batch)
-            loss.backward()
-            torch.cuda.synchronize()
-            if rep == 0:
-                ref_grad, ref_loss = store.grad.clone(), loss.detach().clone()
-                continue
-            same_loss = bool(torch.equal(loss.detach(), ref_loss))
-            if same_loss and torch.equal(store.grad, ref_grad):
-                continue
-            bad_total += 1
-            diff = store.grad != ref_grad
-            params = []
-            for off, (name, n) in sorted(names.items()):
-                cnt = int(diff[off : off + n].sum())
-                if cnt:
-                    delta = float((store.grad[off : off + n] - ref_grad[off : off + n]).abs().max())
-                    params.append({"param": name, "elems": cnt, "of": n, "max_abs": delta})
-            print(json.dumps({"step": step, "rep": rep, "loss_equal": same_loss,
-                              "loss": [float(ref_loss), float(loss)], "params": params}), flush=True)
-        trainer._optimizer_step()
-        if step % 25 == 0:
-            print(json.dumps({"progress": step, "elapsed_s": round(time.perf_counter() - t0, 1)}), flush=True)
+    # the Trainer scopes its kernel policy (run.deterministic) to train_step / fit; this loop
+    # drives the engine directly, so it opens the same scope
+    with trainer.kernel_policy():
+        for step in range(1, args.steps + 1):
+            batch = _to_device(stream.next(), trainer.device)
+            ref_grad = ref_loss = None
+            for rep in range(args.reps):
+                trainer.optimizer.zero_grad()
+                torch.manual_seed(1000 + step)  # the same dropout draw in every repetition
+                with trainer._policy.autocast():
+                    loss, _ = trainer._adapter.compute_loss(trainer.model, batch)
+                loss.backward()
+                torch.cuda.synchronize()
+                if rep == 0:
+                    ref_grad, ref_loss = store.grad.clone(), loss.detach().clone()
+                    continue
+                same_loss = bool(torch.equal(loss.detach(), ref_loss))
+                if same_loss and torch.equal(store.grad, ref_grad):
+                    continue
+                bad_total += 1
+                diff = store.grad != ref_grad
+                params = []
+                for off, (name, n) in sorted(names.items()):
+                    cnt = int(diff[off : off + n].sum())
+                    if cnt:
+                        delta = float((store.grad[off : off + n] - ref_grad[off : off + n]).abs().max())
+                        params.append({"param": name, "elems": cnt, "of": n, "max_abs": delta})
+                print(json.dumps({"step": step, "rep": rep, "loss_equal": same_loss,
+                                  "loss": [float(ref_loss), float(loss)], "params": params}), flush=True)
+            trainer._optimizer_step()
+            if step % 25 == 0:
+                print(json.dumps({"progress": step, "elapsed_s": round(time.perf_counter() - t0, 1)}), flush=True)
     torch.cuda.synchronize()
     print(json.dumps({
         "summary": True, "steps": args.steps, "reps": args.reps, "micro_batch": args.micro_batch,
@@ -106,12 +112,32 @@ def main() -> int:
     return 1 if bad_total else 0
 
 
+def _pollute(gib: float, seed: int) -> None:
+    """Hand the caching allocator ``gib`` GiB of freed blocks holding seed-dependent garbage (random
+    floats, NaN and Inf patterns): the next run's buffers are carved from them, so a read of memory
+    the run never wrote differs from run to run."""
+    g = torch.Generator(device="cuda").manual_seed(1234 + seed)
+    chunks = []
+    for i in range(max(1, int(gib))):
+        t = torch.empty(256 * 2**20, device="cuda")  # 1 GiB
+        t.normal_(generator=g)
+        if i % 4 == 1:
+            t[seed::7] = float("nan")
+        elif i % 4 == 3:
+            t[seed::5] = float("inf")
+        chunks.append(t)
+    torch.cuda.synchronize()
+    del chunks  # back to the allocator's free pool (no empty_cache)
+
+
 def compare_runs(cfg, args: argparse.Namespace) -> int:  # type: ignore[no-untyped-def]
     from llmtrain.training.trainer import Trainer
 
     results = []
     for run in range(args.runs):
         t0 = time.perf_counter()
+        if args.pollute_gib > 0:
+            _pollute(args.pollute_gib, seed=run)
         trainer = Trainer(cfg)
         store = trainer.model.engine.store
         stream = trainer.batch_stream()

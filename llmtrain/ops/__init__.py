@@ -61,16 +61,14 @@ def _on_gpu(t: torch.Tensor) -> bool:
 _POLICY = {"gemm_all_ours": False, "single_stream": False, "deterministic": False}
 
 # How run.deterministic keeps the step bitwise reproducible (LLMTRAIN_DET_SCHEDULE overrides):
-#  * "serial": the weight-gradient GEMMs run on the main stream (no side stream); the LM-head GEMMs
-#    (logits and dX) run on our fixed-order kernel at any size, the other forward / dX GEMMs above
-#    the fused-GEMM size cap stay on hipBLASLt's tuned solutions.  The LM-head dX was measured
-#    non-reproducible on the library (docs/round4.md section 3); the logits moved in round 5 after
-#    one serial run at micro-batch 8 — where they were the only library GEMM — diverged from its
-#    repeat at step 4, although 800 bitwise repeats of that Stream-K kernel (and of the forward
-#    projections' ones) never differed (bench/sk_repeat.py, docs/round5.md).  Evidence for the
+#  * "serial": the weight-gradient GEMMs run on the main stream (no side stream), the forward / dX
+#    GEMMs stay on hipBLASLt's tuned solutions except the LM-head dX (our kernel: the one library
+#    GEMM measured non-reproducible in this schedule, docs/round4.md section 3).  Evidence for the
 #    library GEMMs that remain: bitwise-equal repeats at micro-batch 8 and 32 of GPT-2 124M
-#    (bench/determinism_probe.py, profiles/r4/det/, profiles/r5/det/); other shapes are unpinned,
-#    and each library GEMM of a serial run is named once in the log (_det_library).
+#    (bench/determinism_probe.py, profiles/r4/det/, profiles/r5/det/) and 800 bitwise repeats of the
+#    Stream-K solutions of the LM-head logits and forward projections, alone and beside a
+#    concurrent stream (bench/sk_repeat.py); other shapes are unpinned, and each library GEMM of a
+#    serial run is named once in the log (_det_library).
 #  * "ours": every forward / dX GEMM on the hand-written kernel (csrc/gemm_fused.hip), side stream
 #    kept; slower because that kernel trails hipBLASLt at 128K rows (docs/round4.md).
 DET_SCHEDULES = ("serial", "ours")
@@ -311,8 +309,6 @@ FGEMM_NEVER = frozenset(t for t in os.environ.get("LLMTRAIN_FGEMM_NEVER", "").sp
 # 0.808 ms) but runs 0.86 ms per call inside the step and the step loses 0.4-1.0 % (qkv forward
 # too: -1.2 %; profiles/r3/nt/), so those stay on hipBLASLt.
 FGEMM_ANY_SIZE = frozenset(os.environ.get("LLMTRAIN_FGEMM_ANY", "dx_gelu,dx_attn").split(","))  # A/B knob
-# Ops that take the fused GEMM at any size in deterministic mode (see DET_SCHEDULES)
-_DET_ANY_SIZE = frozenset({"head"})
 
 
 _WARNED: set[str] = set()
@@ -364,8 +360,7 @@ def _fgemm_ok(a: torch.Tensor, k: int, n: int, *others: torch.Tensor | None, op:
     if not (k % 64 == 0 and k >= 256 and n % 8 == 0):
         _det_fallback(f"GEMM {op or 'linear'} K={k} N={n} (needs K % 64 == 0, K >= 256, N % 8 == 0)")
         return False
-    if (a.numel() * a.element_size() > FGEMM_MAX_A_BYTES and op not in FGEMM_ANY_SIZE and not _POLICY["gemm_all_ours"]
-            and not (_POLICY["deterministic"] and op in _DET_ANY_SIZE)):
+    if a.numel() * a.element_size() > FGEMM_MAX_A_BYTES and op not in FGEMM_ANY_SIZE and not _POLICY["gemm_all_ours"]:
         return False
     if op in FGEMM_NEVER and not _POLICY["gemm_all_ours"]:
         return False
@@ -461,10 +456,9 @@ _HEAD_ROWS = 16384
 
 
 def head_logits(h, w):
-    """``logits = h @ w^T`` for the vocab-padded LM head ``w [Vp, d]``: hipBLASLt, or in
-    deterministic mode row chunks of the hand-written GEMM (see DET_SCHEDULES)."""
-    if not (_on_gpu(h) and _POLICY["deterministic"] and h.dtype == torch.bfloat16
-            and _fgemm_ok(h, h.shape[1], w.shape[0], w, op="head")):
+    """``logits = h @ w^T`` for the vocab-padded LM head ``w [Vp, d]``: hipBLASLt, or row chunks
+    of the hand-written GEMM when every GEMM runs on our kernels (deterministic "ours" schedule)."""
+    if not (_on_gpu(h) and _POLICY["gemm_all_ours"] and h.dtype == torch.bfloat16 and _fgemm_ok(h, h.shape[1], w.shape[0], w)):
         return _lib_mm(h, w.t(), op="LM-head logits")
     out = torch.empty(h.shape[0], w.shape[0], dtype=h.dtype, device=h.device)
     for r0 in range(0, h.shape[0], _HEAD_ROWS):

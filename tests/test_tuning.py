@@ -37,18 +37,3 @@ def test_tuned_bias_gemm_shapes_route_to_the_library(monkeypatch) -> None:
     assert not ops._library_tuned_bias_gemm(32768, 3072, 768)  # fc forward at 32: fused GELU epilogue
     assert not ops._library_tuned_bias_gemm(4096, 2304, 768)
 
-
-def test_deterministic_mode_routes_the_lm_head_to_the_fixed_order_gemm() -> None:
-    """run.deterministic: the LM-head logits take the fixed-order fused GEMM at any size (row
-    chunks); the other forward / dX GEMMs above the size cap stay on the library.  Routing only
-    (meta tensors): the GPU tests check the numerics."""
-    from llmtrain import ops
-
-    h = torch.empty(131072, 768, dtype=torch.bfloat16, device="meta")
-    w = torch.empty(50304, 768, dtype=torch.bfloat16, device="meta")
-    with ops.kernel_policy(False):
-        assert not ops._fgemm_ok(h, 768, 50304, w, op="head")  # above the size cap: hipBLASLt
-    with ops.kernel_policy(True, "serial"):
-        assert ops._fgemm_ok(h, 768, 50304, w, op="head")
-        assert not ops._fgemm_ok(h, 768, 2304, w, op="fwd")
-        assert not ops._fgemm_ok(h, 768, 2304, w, op="dx")

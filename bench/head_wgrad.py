@@ -5,8 +5,7 @@
 
   * addmm_fp32: ``dW(fp32) += dlogits^T hf`` via ``addmm(out_dtype=fp32)`` (the engine's default)
   * mm_bf16_add: bf16-output GEMM (TunableOp-eligible) + fp32 add (torch autocast numerics)
-  * wgrad_hip:   the split-K MFMA weight-gradient kernel (csrc/gemm_wgrad.hip) into dW
-  * wgrad_hip_pipe: the same, software-pipelined kernel (the engine's LM-head choice)
+  * wgrad_hip:   the weight-gradient kernel (csrc/gemm_wgrad_pp.hip) into dW (the engine's choice)
   * hfT_mm_fp32 / hfT_mm_bf16: dW^T = hf^T dlogits with hf^T materialised (K-contiguous A, the
     "NN" class hipBLASLt runs at ~1.7 PF for the head dX), fp32 / bf16 output, + transpose-add
 Prints ms and PFLOP/s per variant, and the max error of each against an fp64-accumulated check
@@ -61,7 +60,6 @@ def main() -> int:
         "addmm_fp32": lambda: accumulate_wgrad(dw, dy, hf),
         "mm_bf16_add": lambda: dw.add_(torch.mm(dy.t(), hf)),
         "wgrad_hip": lambda: ops.wgrad_accum(dw, dy, hf),
-        "wgrad_hip_pipe": lambda: ops.wgrad_accum(dw, dy, hf, exclusive=True),
         "hfT_mm_fp32": lambda: dw.add_(torch.mm(hf.t().contiguous(), dy, out_dtype=torch.float32).t()),
         "hfT_mm_bf16": lambda: dw.add_(torch.mm(hf.t().contiguous(), dy).t()),
         "hfT_only_mm_bf16": lambda: torch.mm(hfT, dlogits),

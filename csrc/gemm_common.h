@@ -1,4 +1,4 @@
-// Building blocks shared by the gfx950 MFMA GEMM kernels (gemm_wgrad.hip, gemm_fused.hip):
+// Building blocks shared by the gfx950 MFMA GEMM kernels (gemm_wgrad_pp.hip, gemm_fused.hip):
 // LDS-DMA staging (`buffer_load_dwordx4 ... lds`), counted vmcnt + raw barrier stage waits,
 // XOR-swizzled LDS images and the fragment readers for v_mfma_f32_32x32x16_bf16.
 #pragma once

@@ -1,7 +1,7 @@
 // Weight-gradient GEMM, ping-pong schedule (gfx950):  C[N, K] (f32) += A^T B
 //   A = dY [M, N] bf16 row-major (lda), B = X [M, K] bf16 row-major (ldb), reduction over M.
 //
-// The round-3 kernels (gemm_wgrad.hip) run one wave per SIMD: each wave issues its own LDS-DMA
+// The round-3 kernels (deleted in round 5) ran one wave per SIMD: each wave issues its own LDS-DMA
 // fill, its transposed fragment reads and then its MFMAs, so the matrix pipe idles whenever the
 // wave waits (45 % MFMA-busy, profiles/r2/pmc_wgrad_qkv_plain.txt); the software-pipelined variant
 // fixes that but needs all 512 registers.  Here each SIMD hosts TWO waves of one 512-thread
@@ -30,7 +30,7 @@
 //    the swizzle is applied to the per-lane DMA source address because LDS-DMA writes lane-linear.
 //
 // Epilogues (MODE): 0 = plain 16-byte stores of the tile into its own fp32 slab; a second pass
-// (wgrad_slab_reduce_kernel) adds the split slabs to C in chunk order — deterministic, and cheaper
+// (wgrad_finish_kernel) adds the split slabs to C in chunk order — deterministic, and cheaper
 // than fp32 atomics at ~1.3 TB/s for these 64-256 MB of partials.  1 = C += acc read-modify-write
 // (split == 1: each element has one owner, no atomics).  2 = fp32 atomics (huge outputs whose
 // slabs would not pay, fast mode only).

@@ -150,17 +150,22 @@ def _reducer_worker(rank: int, world: int, port: int, out_dir: str) -> None:
     dist.destroy_process_group()
 
 
-def test_flat_reducer_averages_gradients(tmp_path: Path) -> None:
-    mp.spawn(_reducer_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
-    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
-    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
-    assert torch.equal(r0["params"], r1["params"])  # broadcast at wrap time
-    assert torch.allclose(r0["grad"], r1["grad"])
+@pytest.mark.parametrize("world", [2, 4])
+def test_flat_reducer_averages_gradients(tmp_path: Path, world: int) -> None:
+    """The flat bucketed reducer at 2 and 4 gloo ranks (the 8-GPU path's logic beyond one pair):
+    rank 0's parameters broadcast at wrap time, every rank ends with the average of all ranks'
+    gradients, and the bucket-wise norm equals the global one."""
+    mp.spawn(_reducer_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    ranks = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
+    r0 = ranks[0]
+    for other in ranks[1:]:
+        assert torch.equal(r0["params"], other["params"])  # broadcast at wrap time
+        assert torch.allclose(r0["grad"], other["grad"])
     # reference: per-rank gradients computed independently, then averaged
     from llmtrain.models.gpt import GPT
 
     grads = []
-    for rank_data in (r0, r1):
+    for rank_data in ranks:
         model = GPT(vocab_size=50, block_size=8, d_model=64, n_layers=2, n_heads=2, d_ff=64, dropout=0.0)
         model.prepare_runtime(compute_dtype=torch.float32)
         with torch.no_grad():
@@ -170,7 +175,7 @@ def test_flat_reducer_averages_gradients(tmp_path: Path) -> None:
         for b in rank_data["batches"]:
             (model.fused_loss(b, b) / 2).backward()
         grads.append(model.flat_store.grad.clone())
-    torch.testing.assert_close(r0["grad"], (grads[0] + grads[1]) / 2, atol=1e-6, rtol=1e-5)
+    torch.testing.assert_close(r0["grad"], sum(grads) / world, atol=1e-6, rtol=1e-5)
 
 
 def _trainer_worker(rank: int, world: int, port: int, out_dir: str, fused: bool) -> None:

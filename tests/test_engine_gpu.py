@@ -56,6 +56,10 @@ PRESET_SHAPES = {
     "gpt_wikitext_ddp": (50257, 128, 256, 4, 4, 1024),  # head dim 64
     "gpt_wikitext_better": (50257, 256, 384, 12, 8, 1536),  # head dim 48
     "head_dim_128": (50257, 256, 512, 4, 4, 2048),  # not a reference preset: the hd = 128 kernels
+    # not a reference preset: two GPT-2 XL blocks (BASELINE config 5's shapes: d 1600, 25 heads,
+    # d_ff 6400; at B = 4 the fused GEMMs take every forward / dX projection and the attention
+    # backward its split grid)
+    "gpt2_xl_blocks": (50257, 1024, 1600, 2, 25, 6400),
 }
 
 

@@ -148,7 +148,9 @@ __device__ __forceinline__ void dma_stage(unsigned dst_a, unsigned dst_b, const 
       : [da] "s"(dst_a), [db] "s"(dst_b), [a0] "v"(va[0]), [a1] "v"(va[1]), [a2] "v"(va[2]), [a3] "v"(va[3]),
         [b0] "v"(vb[0]), [b1] "v"(vb[1]), [b2] "v"(vb[2]), [b3] "v"(vb[3]), [ra] "s"(ra), [rb] "s"(rb),
         [soa] "s"(soa), [sob] "s"(sob)
-      : "memory");
+      // s_add_u32 writes SCC: left undeclared, the compiler may branch on a flag it set before the
+      // asm (a BK = 32 variant of this kernel did exactly that and re-loaded stage 0; round5 §13)
+      : "memory", "scc");
 }
 
 // Wait for the newest issued stage (nothing was issued after it but, when `post`, an epilogue's

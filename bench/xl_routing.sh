@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# GPT-2 XL (BASELINE config 5, the gpt2_xl_mi355x_ddp8 preset's shape: micro-batch 16 x 4,
+# GPT-2 XL (BASELINE config 5, micro-batch 16 x 4, the gpt2_xl_mi355x_ddp8 preset's shape until it moved to 32 x 2,
 # run.deterministic) GEMM routing study on one GPU box:
 #  1) a TunableOp pass with every forward / dX GEMM sent to the library (so each shape gets a
 #     measured hipBLASLt / rocBLAS solution), table -> OUT/tuned_xl.csv;

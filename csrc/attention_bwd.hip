@@ -9,9 +9,9 @@
 //    32w..32w+31 with the KEY ON THE MFMA LANE: its K and V fragments stay in registers and its
 //    dK^T / dV^T accumulators (2 x 32x32 f32 tiles each) live in registers for the whole sweep
 //    over query tiles, so dK and dV need no cross-workgroup reduction;
-//  * per 32-row query tile: S = Q K^T and dP = dO V^T with the accumulators PRE-LOADED with the
-//    row constants (-LSE/scale and -delta) so exp2(c*S) is P directly and dP - delta comes out
-//    of the MFMA chain; dS = P o (dP - delta);
+//  * per 32-row query sub-tile: S = Q K^T and dP = dO V^T from zero accumulators, then
+//    P = exp2(fma(S, scale*log2e, -lse*log2e)) and dP - delta, the row constants read from LDS
+//    after the MFMA chains; dS = P o (dP - delta);
 //  * P and dS are already the B operands of dV^T += dO^T P and dK^T += Q^T dS (accumulator used
 //    as the next MFMA's operand); dO^T and Q^T fragments come from ds_read_b64_tr_b16 on the
 //    same LDS images that serve the row reads (one swizzle, conflict free both ways);

@@ -64,8 +64,9 @@ _POLICY = {"gemm_all_ours": False, "single_stream": False, "deterministic": Fals
 #  * "serial": the weight-gradient GEMMs run on the main stream (no side stream), the forward / dX
 #    GEMMs stay on hipBLASLt's tuned solutions except the LM-head dX (our kernel: the one library
 #    GEMM measured non-reproducible in this schedule, docs/round4.md section 3).  Evidence for the
-#    library GEMMs that remain: bitwise-equal repeats at micro-batch 8 and 32 of GPT-2 124M
-#    (bench/determinism_probe.py, profiles/r4/det/, profiles/r5/det/) and 800 bitwise repeats of the
+#    library GEMMs that remain: bitwise-equal repeats at micro-batch 8 and 32 of GPT-2 124M and
+#    at micro-batch 32 of GPT-2 XL (the XL preset; 3 whole runs x 20 steps) (bench/determinism_probe.py,
+#    profiles/r4/det/, profiles/r5/det/) and 800 bitwise repeats of the
 #    Stream-K solutions of the LM-head logits and forward projections, alone and beside a
 #    concurrent stream (bench/sk_repeat.py); other shapes are unpinned, and each library GEMM of a
 #    serial run is named once in the log (_det_library).
@@ -333,8 +334,9 @@ def _det_fallback(what: str, always: bool = False) -> None:
 
 def _det_library(what: str) -> None:
     """Serial deterministic schedule: ``what`` runs on a tuned hipBLASLt solution by design.  Those
-    were bitwise reproducible in every repeat measured (GPT-2 124M at micro-batch 8 and 32,
-    profiles/r4/det/), which pins no other shape: name each such GEMM once in the log, so a run on a
+    were bitwise reproducible in every repeat measured (GPT-2 124M at micro-batch 8 and 32, GPT-2 XL
+    at 32; profiles/r4/det/, profiles/r5/det/), which pins no other shape: name each such GEMM once
+    in the log, so a run on a
     new shape knows which of its GEMMs rest on that evidence (LLMTRAIN_DET_SCHEDULE=ours moves every
     one the kernel can take onto the fixed-order kernel)."""
     if _POLICY["single_stream"] and what not in _WARNED:
@@ -343,7 +345,7 @@ def _det_library(what: str) -> None:
 
         logging.getLogger(__name__).warning(
             "run.deterministic (serial schedule): %s runs on hipBLASLt; its reproducibility is measured "
-            "for GPT-2 124M at micro-batch 8/32 only", what,
+            "for GPT-2 124M at micro-batch 8/32 and GPT-2 XL at 32 only", what,
         )
 
 

@@ -114,12 +114,17 @@ def sweep(model: str, M: int, splits: str, mode: int) -> None:
     quantisation and the slab traffic of the split epilogue cost."""
     ops = _ops()
     _warm()
+    first = True
     for name, (N, K) in SHAPES[model].items():
         lda = 50304 if N == 50257 else N
         dy = torch.randn(M, lda, device="cuda", dtype=torch.bfloat16)[:, :N]
         x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
         acc = torch.zeros(N, K, device="cuda")
         flops = 2.0 * M * N * K
+        if first:  # the first timing of a process reads high even after _warm (profiles/r5/xl/
+            # sweep_split_xl_m32k.jsonl: qkv auto 0.62 ms, the same split later 0.55): time it once, unreported
+            timeit(lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, mode))
+            first = False
         for s in (int(v) for v in splits.replace("+", ",").split(",")):
             ms = timeit(lambda: ops.wgrad_gemm_pp(dy, x, acc, None, s, mode))
             print(json.dumps({"model": model, "M": M, "gemm": name, "split": s, "mode": mode, "ms": round(ms, 4),

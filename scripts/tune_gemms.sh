@@ -3,13 +3,16 @@
 # shipped table (llmtrain/runtime/tuned/), then (AB=1) A/B the bench with and without the table on
 # the same box.  New table: gpurun_out/tunableop/tuned0.csv (the shipped rows + the new shapes).
 #   BENCH_ARGS="--model gpt2-xl --micro-batch 16 --grad-accum 2" AB=0 bash scripts/tune_gemms.sh
+# FRESH=1: re-tune every shape from an empty table, and A/B it against the shipped table instead
+# of the library heuristics (e.g. with PYTORCH_TUNABLEOP_ROTATING_BUFFER_SIZE=1024, so candidates
+# are timed on operands that are not cache-resident, as in the step).
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/tunableop
 mkdir -p "$OUT"
 MB=${MB:-128}
-cp llmtrain/runtime/tuned/gemm_tunableop_gfx950.csv "$OUT/tuned0.csv"
+if [ "${FRESH:-0}" = 1 ]; then rm -f "$OUT/tuned0.csv"; else cp llmtrain/runtime/tuned/gemm_tunableop_gfx950.csv "$OUT/tuned0.csv"; fi
 # a heartbeat on stdout while the tuning pass runs (it prints nothing for minutes at a time)
 ( while sleep 50; do echo "tuning... $(wc -l < "$OUT/tune.log" 2>/dev/null || echo 0) log lines"; done ) &
 HB=$!
@@ -27,8 +30,9 @@ cat "$OUT"/tuned0.csv
 # 2) same-box A/B: library heuristics vs the tuned table (tuning off, look-ups only)
 for round in 1 2; do
   for tag in base tuned; do
-    if [ "$tag" = tuned ]; then envs="PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=0 PYTORCH_TUNABLEOP_FILENAME=$OUT/tuned%d.csv"; else envs="LLMTRAIN_TUNED_GEMMS=0"; fi
-    env $envs timeout -k 10 300 python bench.py --steps 20 --warmup 5 --micro-batch "$MB" ${BENCH_ARGS:-} \
+    if [ "$tag" = tuned ]; then envs="PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=0 PYTORCH_TUNABLEOP_FILENAME=$OUT/tuned%d.csv"
+    elif [ "${FRESH:-0}" = 1 ]; then envs="LLMTRAIN_TUNED_GEMMS=1"; else envs="LLMTRAIN_TUNED_GEMMS=0"; fi
+    env -u PYTORCH_TUNABLEOP_ROTATING_BUFFER_SIZE $envs timeout -k 10 300 python bench.py --steps 20 --warmup 5 --micro-batch "$MB" ${BENCH_ARGS:-} \
       > "$OUT/bench_${tag}_${round}.log" 2>&1 || { echo "bench $tag failed"; tail -20 "$OUT/bench_${tag}_${round}.log"; exit 1; }
     echo "$tag round$round: $(tail -1 "$OUT/bench_${tag}_${round}.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
   done

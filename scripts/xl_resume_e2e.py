@@ -31,8 +31,8 @@ RUNS = Path(os.environ.get("TMPDIR", "/tmp")) / "llmtrain_xl_e2e_runs"
 def _config(out: Path, name: str, fail_at: int | None) -> Path:
     cfg = yaml.safe_load((REPO / "configs/presets/gpt2_xl_mi355x_ddp8.yaml").read_text())
     cfg["run"]["name"] = name
-    cfg["trainer"].update(max_steps=6, save_every_steps=4, log_every_steps=1, eval_every_steps=1000, warmup_steps=2,
-                          micro_batch_size=16, grad_accum_steps=2)
+    # the preset's own micro-batch x grad-accum (32 x 2 since round 5)
+    cfg["trainer"].update(max_steps=6, save_every_steps=4, log_every_steps=1, eval_every_steps=1000, warmup_steps=2)
     cfg["trainer"]["extra"] = {"keep_last_k": 1, "bucket_cap_mb": 128}
     if fail_at is not None:
         cfg["trainer"]["extra"]["fail_at_step"] = fail_at

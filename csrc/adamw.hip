@@ -5,7 +5,11 @@
 // both moments AND the bf16 shadow copy of the weights used by the next forward's GEMMs
 // (30 B per parameter, HBM bound).  The gradient-clipping coefficient arrives as a device
 // scalar (computed from the sumsq kernel below), so clipping costs no host round trip and
-// no extra pass over the gradients.  The update order matches torch.optim.AdamW exactly:
+// no extra pass over the gradients.  A non-finite coefficient (clip_coef_kernel below makes it NaN
+// when the global gradient norm is NaN/Inf) skips the whole update on device: every workgroup
+// returns before its first store, so weights, moments and shadow keep the last good step, and one
+// lane bumps the skipped-step counters {total, consecutive} (no poisoned state, no
+// host sync).  The update order matches torch.optim.AdamW exactly:
 //   p *= 1 - lr*wd;  m += (1-b1)(g-m);  v = b2 v + (1-b2) g^2;
 //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
 
@@ -27,13 +31,31 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p -= s.step_size * (m / denom);
 }
 
+// Non-finite clip coefficient: the step is skipped by every workgroup (uniform branch).  Block 0's
+// first lane keeps the counters: skipped[0] = steps skipped in total, skipped[1] = consecutive
+// skips (reset by an applied step).  Plain vector stores from one lane, no atomics.
+__device__ __forceinline__ bool adamw_skip(float gs, int* __restrict__ skipped) {
+  const bool skip = !isfinite(gs);
+  if (skipped != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+    if (skip) {
+      skipped[0] += 1;
+      skipped[1] += 1;
+    } else {
+      skipped[1] = 0;
+    }
+  }
+  return skip;
+}
+
 template <bool SHADOW_BF16>
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ param, const float* __restrict__ grad,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     void* __restrict__ shadow,
                                                     const float* __restrict__ grad_scale, long n,
-                                                    AdamScalars s, const float* __restrict__ dyn) {
+                                                    AdamScalars s, const float* __restrict__ dyn,
+                                                    int* __restrict__ skipped) {
   const float gs = grad_scale != nullptr ? *grad_scale : 1.f;
+  if (adamw_skip(gs, skipped)) return;
   if (dyn != nullptr) {  // graph replay: this step's scalars from device memory
     s.decay = dyn[0];
     s.step_size = dyn[1];
@@ -97,9 +119,11 @@ __global__ __launch_bounds__(256) void adamw_tiled_kernel(float* __restrict__ pa
                                                           float* __restrict__ m, float* __restrict__ v,
                                                           void* __restrict__ shadow,
                                                           const float* __restrict__ grad_scale, long n4,
-                                                          AdamScalars s, const float* __restrict__ dyn) {
+                                                          AdamScalars s, const float* __restrict__ dyn,
+                                                          int* __restrict__ skipped) {
   constexpr int kU = 2;
   const float gs = grad_scale != nullptr ? *grad_scale : 1.f;
+  if (adamw_skip(gs, skipped)) return;
   if (dyn != nullptr) {
     s.decay = dyn[0];
     s.step_size = dyn[1];
@@ -184,6 +208,16 @@ __global__ __launch_bounds__(kSumsqThreads) void sumsq_final_kernel(const float*
   if (threadIdx.x == 0) *out = acc;
 }
 
+// {norm, coef} of clip_grad_norm_ from the global squared norm: norm = sqrt(sumsq),
+// coef = min(1, max_norm / (norm + 1e-6)), and coef = NaN when norm is NaN/Inf (an Inf norm would
+// otherwise give coef 0, and 0 * Inf gradients NaN), which makes the AdamW kernels skip the step.
+__global__ void clip_coef_kernel(const float* __restrict__ sumsq, float max_norm, float* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  const float norm = sqrtf(*sumsq);
+  out[0] = norm;
+  out[1] = isfinite(norm) ? fminf(max_norm / (norm + 1e-6f), 1.f) : __builtin_nanf("");
+}
+
 }  // namespace
 
 void adamw_step_scalars(const AdamWArgs& a, float out[3]) {
@@ -211,25 +245,30 @@ hipError_t launch_adamw_flat(const AdamWArgs& a, hipStream_t stream) {
     const long blocks = (n4 + 511) / 512;
     if (a.shadow_bf16)
       hipLaunchKernelGGL(adamw_tiled_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, a.param, a.grad,
-                         a.exp_avg, a.exp_avg_sq, a.shadow, a.grad_scale, n4, s, a.dyn);
+                         a.exp_avg, a.exp_avg_sq, a.shadow, a.grad_scale, n4, s, a.dyn, a.skipped);
     else
       hipLaunchKernelGGL(adamw_tiled_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, a.param, a.grad,
-                         a.exp_avg, a.exp_avg_sq, a.shadow, a.grad_scale, n4, s, a.dyn);
+                         a.exp_avg, a.exp_avg_sq, a.shadow, a.grad_scale, n4, s, a.dyn, a.skipped);
     return hipGetLastError();
   }
   const int grid = stride_grid((a.n + 3) / 4, 256, 256 * 8);
   if (a.shadow_bf16)
     hipLaunchKernelGGL(adamw_kernel<true>, dim3(grid), dim3(256), 0, stream, a.param, a.grad, a.exp_avg,
-                       a.exp_avg_sq, a.shadow, a.grad_scale, (long)a.n, s, a.dyn);
+                       a.exp_avg_sq, a.shadow, a.grad_scale, (long)a.n, s, a.dyn, a.skipped);
   else
     hipLaunchKernelGGL(adamw_kernel<false>, dim3(grid), dim3(256), 0, stream, a.param, a.grad, a.exp_avg,
-                       a.exp_avg_sq, a.shadow, a.grad_scale, (long)a.n, s, a.dyn);
+                       a.exp_avg_sq, a.shadow, a.grad_scale, (long)a.n, s, a.dyn, a.skipped);
   return hipGetLastError();
 }
 
 hipError_t launch_sumsq(const float* x, long long n, float* partials, float* out, hipStream_t stream) {
   hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kSumsqBlocks), dim3(kSumsqThreads), 0, stream, x, (long)n, partials);
   hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(kSumsqThreads), 0, stream, partials, kSumsqBlocks, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_clip_coef(const float* sumsq, float max_norm, float* out, hipStream_t stream) {
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(64), 0, stream, sumsq, max_norm, out);
   return hipGetLastError();
 }
 

@@ -603,7 +603,8 @@ Tensor sumsq(const Tensor& x) {
 
 void adamw_flat(Tensor param, const Tensor& grad, Tensor exp_avg, Tensor exp_avg_sq, const c10::optional<Tensor>& shadow,
                 double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
-                const c10::optional<Tensor>& grad_scale, const c10::optional<Tensor>& dyn) {
+                const c10::optional<Tensor>& grad_scale, const c10::optional<Tensor>& dyn,
+                const c10::optional<Tensor>& skipped) {
   for (const Tensor* t : {static_cast<const Tensor*>(&param), &grad, static_cast<const Tensor*>(&exp_avg),
                           static_cast<const Tensor*>(&exp_avg_sq)}) {
     check_gpu(*t, "adamw buffer");
@@ -642,7 +643,25 @@ void adamw_flat(Tensor param, const Tensor& grad, Tensor exp_avg, Tensor exp_avg
     TORCH_CHECK(dyn->numel() == 3 && dyn->is_contiguous(), "adamw dyn scalars: 3 contiguous floats");
     a.dyn = dyn->data_ptr<float>();
   }
+  if (skipped.has_value()) {
+    check_gpu(*skipped, "adamw skipped-step counters");
+    check_dtype(*skipped, at::kInt, "adamw skipped-step counters");
+    TORCH_CHECK(skipped->numel() == 2 && skipped->is_contiguous(), "adamw skipped-step counters: 2 contiguous int32");
+    a.skipped = skipped->data_ptr<int>();
+  }
   check_hip(llmt::launch_adamw_flat(a, cur_stream()), "adamw_flat");
+}
+
+// [norm, coef] of the gradient clip from the global squared norm (coef NaN when norm is not finite)
+Tensor clip_coef(const Tensor& sumsq, double max_norm) {
+  check_gpu(sumsq, "sumsq");
+  check_dtype(sumsq, at::kFloat, "sumsq");
+  TORCH_CHECK(sumsq.numel() == 1, "clip_coef: sumsq must be one float");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(sumsq.device());
+  Tensor out = at::empty({2}, sumsq.options());
+  check_hip(llmt::launch_clip_coef(sumsq.data_ptr<float>(), (float)max_norm, out.data_ptr<float>(), cur_stream()),
+            "clip_coef");
+  return out;
 }
 
 // {decay, step_size, bc2_sqrt} of one AdamW step exactly as adamw_flat forms them (CPU tensor): the
@@ -696,7 +715,8 @@ TORCH_LIBRARY(llmtrain_hip, m) {
   m.def("sumsq(Tensor x) -> Tensor");
   m.def("adamw_flat(Tensor(a!) param, Tensor grad, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor(d!)? shadow,"
         " float lr, float beta1, float beta2, float eps, float weight_decay, int step, Tensor? grad_scale,"
-        " Tensor? dyn=None) -> ()");
+        " Tensor? dyn=None, Tensor(e!)? skipped=None) -> ()");
+  m.def("clip_coef(Tensor sumsq, float max_norm) -> Tensor");
   m.def("adamw_stage_scalars(float lr, float beta1, float beta2, float eps, float weight_decay, int step) -> Tensor",
         &adamw_stage_scalars);
 }
@@ -720,4 +740,5 @@ TORCH_LIBRARY_IMPL(llmtrain_hip, CUDA, m) {
   m.impl("gemm_fused", &gemm_fused);
   m.impl("sumsq", &sumsq);
   m.impl("adamw_flat", &adamw_flat);
+  m.impl("clip_coef", &clip_coef);
 }

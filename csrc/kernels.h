@@ -133,6 +133,9 @@ struct AdamWArgs {
   // optional device [decay, step_size, bc2_sqrt]: per-step scalars staged by the host before a
   // hipGraph replay of the training step (the by-value ones above would be baked into the graph)
   const float* dyn;
+  // optional device int32 {total, consecutive} skipped-step counters; a non-finite *grad_scale
+  // skips the update (nothing written) and bumps both, an applied step resets the second
+  int* skipped;
 };
 hipError_t launch_adamw_flat(const AdamWArgs& a, hipStream_t stream);
 // the three per-step scalars exactly as launch_adamw_flat forms them: {decay, step_size, bc2_sqrt}
@@ -141,6 +144,9 @@ void adamw_step_scalars(const AdamWArgs& a, float out[3]);
 constexpr int kSumsqBlocks = 1024;
 hipError_t launch_sumsq(const float* x, long long n, float* partials, float* out,
                         hipStream_t stream);
+// out[0] = sqrt(*sumsq) (global gradient norm), out[1] = min(1, max_norm / (out[0] + 1e-6)), NaN
+// when the norm is not finite (the AdamW kernels then skip the step)
+hipError_t launch_clip_coef(const float* sumsq, float max_norm, float* out, hipStream_t stream);
 
 // Ping-pong weight-gradient GEMM (gemm_wgrad_pp.hip): C[N,K] += dy^T x and, with `bias`,
 // bias[N] += colsum(dy).  `ws` holds wgrad_pp_ws_floats(...) floats (split slabs + bias parts).

@@ -23,6 +23,7 @@ __all__ = [
     "attn_bwd",
     "attn_fwd",
     "attn_key_masks",
+    "clip_coef",
     "colsum_accum",
     "cross_entropy_fwd_bwd",
     "embedding_bwd",
@@ -542,19 +543,32 @@ def sumsq(x):
     return ref.sumsq(x)
 
 
+def clip_coef(sumsq_t, max_norm: float):
+    """``[norm, coef]`` of the gradient clip from the global squared norm (fp32, one element):
+    ``norm = sqrt(sumsq)``, ``coef = min(1, max_norm / (norm + 1e-6))`` (``clip_grad_norm_``), and
+    ``coef = NaN`` when the norm is NaN/Inf, which makes :func:`adamw_flat` skip the step."""
+    if _on_gpu(sumsq_t):
+        return hip_ops().clip_coef(sumsq_t.reshape(1).float(), float(max_norm))
+    return ref.clip_coef(sumsq_t, max_norm)
+
+
 def adamw_flat(
-    param, grad, exp_avg, exp_avg_sq, shadow, *, lr, beta1, beta2, eps, weight_decay, step, grad_scale, dyn=None
+    param, grad, exp_avg, exp_avg_sq, shadow, *, lr, beta1, beta2, eps, weight_decay, step, grad_scale, dyn=None,
+    skipped=None,
 ):
     """``dyn`` (GPU only): device ``[decay, step_size, bc2_sqrt]`` read by the kernel instead of the
-    values formed from ``lr``/``step`` — a hipGraph-captured step stages them before each replay."""
+    values formed from ``lr``/``step`` — a hipGraph-captured step stages them before each replay.
+    A non-finite ``grad_scale`` skips the update (nothing is written); ``skipped`` (int32 ``[2]``,
+    optional) then counts it: ``[total, consecutive]``, the second reset by an applied step."""
     if _on_gpu(param):
         hip_ops().adamw_flat(
-            param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps, weight_decay, step, grad_scale, dyn
+            param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps, weight_decay, step, grad_scale, dyn,
+            skipped,
         )
         return
     if dyn is not None:
         raise ValueError("adamw_flat: device-staged scalars exist only on the GPU path")
     ref.adamw_flat(
         param, grad, exp_avg, exp_avg_sq, shadow, lr=lr, beta1=beta1, beta2=beta2, eps=eps,
-        weight_decay=weight_decay, step=step, grad_scale=grad_scale,
+        weight_decay=weight_decay, step=step, grad_scale=grad_scale, skipped=skipped,
     )

@@ -21,6 +21,7 @@ import torch.nn.functional as F
 
 __all__ = [
     "adamw_flat",
+    "clip_coef",
     "dropout_keep",
     "dropout_params",
     "dropout_site_seed",
@@ -313,6 +314,14 @@ def sumsq(x: torch.Tensor) -> torch.Tensor:
     return x.float().pow(2).sum()
 
 
+def clip_coef(sumsq_t: torch.Tensor, max_norm: float) -> torch.Tensor:
+    """``[norm, coef]``: ``coef = min(1, max_norm / (norm + 1e-6))``, NaN for a non-finite norm."""
+    norm = torch.sqrt(sumsq_t.float().reshape(1))
+    coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+    coef = torch.where(torch.isfinite(norm), coef, torch.full_like(coef, float("nan")))
+    return torch.cat([norm, coef])
+
+
 def adamw_flat(
     param: torch.Tensor,
     grad: torch.Tensor,
@@ -327,13 +336,22 @@ def adamw_flat(
     weight_decay: float,
     step: int,
     grad_scale: torch.Tensor | None,
+    skipped: torch.Tensor | None = None,
 ) -> None:
     """One decoupled-weight-decay Adam step over flat fp32 buffers (torch.optim.AdamW math).
 
     ``grad_scale`` (0-d fp32) multiplies the gradient first (gradient clipping without a host
     sync). When ``shadow`` is given, the updated parameters are also written to it (bf16 copy
     used by the compute path); ``shadow`` may be longer than ``param`` (padding is untouched).
+    A non-finite ``grad_scale`` skips the step; ``skipped`` (int32 ``[total, consecutive]``)
+    counts skips like the HIP kernel.
     """
+    if grad_scale is not None and not bool(torch.isfinite(grad_scale).all()):
+        if skipped is not None:
+            skipped += 1
+        return
+    if skipped is not None:
+        skipped[1] = 0
     g = grad if grad_scale is None else grad * grad_scale
     param.mul_(1.0 - lr * weight_decay)
     exp_avg.lerp_(g, 1.0 - beta1)

@@ -11,6 +11,13 @@ HIP kernel over the flat buffers: it reads the fp32 master weight, gradient and 
 applies the (device-side) gradient-clipping coefficient, writes the new master weight, both
 moments AND the bf16 shadow copy used by the next forward — one HBM pass, no per-tensor
 launches, no host sync.
+
+Non-finite gradients: :func:`fused_clip_coef` turns a NaN/Inf global norm into a
+NaN clip coefficient, and the AdamW kernel then skips the whole update on device — master
+weights, both moments and the shadow keep the last good step — and bumps the int32 counters
+:attr:`FusedAdamW.skipped` ``[total, consecutive]``.  The Trainer reads them at its log / save
+cadence (already host-sync points).  A skipped step still advances the step counter and the LR
+schedule (the host cannot know without a sync), so a resumed run replays it identically.
 """
 
 from __future__ import annotations
@@ -62,6 +69,8 @@ class FusedAdamW(torch.optim.Optimizer):
         self._step_count_host = 0
         self._step_tensor = torch.zeros((), dtype=torch.float32)
         self._dyn: torch.Tensor | None = None  # device per-step scalars of a graph-captured step
+        # device int32 [total, consecutive] steps skipped for a non-finite gradient norm
+        self.skipped = torch.zeros(2, dtype=torch.int32, device=store.master.device)
 
     # -- torch-compatible state -----------------------------------------------------------
 
@@ -140,6 +149,7 @@ class FusedAdamW(torch.optim.Optimizer):
             weight_decay=float(group["weight_decay"]),
             step=self._step_count_host,
             grad_scale=grad_scale,
+            skipped=self.skipped,
         )
         self.store.mark_shadow_synced()
         return loss
@@ -181,7 +191,7 @@ class FusedAdamW(torch.optim.Optimizer):
             self.store.master, self.store.grad, self.exp_avg, self.exp_avg_sq, self.store.shadow,
             lr=float(group["lr"]), beta1=float(beta1), beta2=float(beta2), eps=float(group["eps"]),
             weight_decay=float(group["weight_decay"]), step=max(1, self._step_count_host), grad_scale=grad_scale,
-            dyn=self._dyn,
+            dyn=self._dyn, skipped=self.skipped,
         )
         self.store.mark_shadow_synced()
 
@@ -189,12 +199,13 @@ class FusedAdamW(torch.optim.Optimizer):
 def fused_clip_coef(
     store: Any, max_norm: float, *, sumsq: torch.Tensor | None = None
 ) -> tuple[torch.Tensor, torch.Tensor]:
-    """Global grad L2 norm and ``min(1, max_norm / (norm + 1e-6))``, both as device scalars.
-    ``sumsq``: the squared norm already summed elsewhere (the data-parallel reducer's per-bucket
-    partials, :meth:`FlatDataParallel.grad_sumsq`) instead of a pass over ``store.grad``."""
-    total = torch.sqrt(ops.sumsq(store.grad) if sumsq is None else sumsq)
-    coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
-    return total, coef
+    """Global grad L2 norm and ``min(1, max_norm / (norm + 1e-6))``, both as device scalars (one
+    HIP launch after the squared-norm reduction); the coefficient is NaN when the norm is NaN/Inf,
+    which makes the fused AdamW skip the step.  ``sumsq``: the squared norm already summed elsewhere
+    (the data-parallel reducer's per-bucket partials, :meth:`FlatDataParallel.grad_sumsq`) instead of
+    a pass over ``store.grad``."""
+    out = ops.clip_coef(ops.sumsq(store.grad) if sumsq is None else sumsq, max_norm)
+    return out[0], out[1]
 
 
 def build_optimizer(model: nn.Module, lr: float, weight_decay: float) -> torch.optim.Optimizer:

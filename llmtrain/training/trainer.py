@@ -25,7 +25,15 @@ What changes on the MI355X path:
   eager steps the whole optimizer step is captured once as a hipGraph and replayed
   (:mod:`llmtrain.training.graph_step`) — for the launch-bound small presets;
 * ``train/allreduce_ms`` (max over ranks) logs the exposed gradient all-reduce time of the flat
-  reducer — the part of the communication NOT hidden behind the backward.
+  reducer — the part of the communication NOT hidden behind the backward;
+* non-finite gradients (the reference clips, steps and saves unconditionally,
+  ``training/trainer.py:390-413``): a NaN/Inf global gradient norm skips the optimizer update
+  (on device for the fused AdamW, no host sync), ``train/skipped_steps`` counts them at the log
+  cadence (once one was skipped), ``trainer.extra.max_skipped_steps`` (default 8) consecutive skips seen at a log / save
+  step raise, and a checkpoint is never written from non-finite weights or moments — the K8s
+  auto-resume therefore never restarts from poisoned state.  ``trainer.extra.
+  inject_nonfinite_grad_at_step`` (+ ``inject_nonfinite_rank``, default every rank) poisons that
+  step's backward with NaN for fault-injection tests.
 """
 
 from __future__ import annotations
@@ -212,6 +220,11 @@ class Trainer:
                 f"{cfg.trainer.save_every_steps} (a restart must find a checkpoint to resume from)"
             )
         self.last_grad_norm: torch.Tensor | None = None
+        self._skipped_host = [0, 0]  # module path: [total, consecutive] skipped steps
+        self._max_skipped = int(cfg.trainer.extra.get("max_skipped_steps", 8))
+        inject = cfg.trainer.extra.get("inject_nonfinite_grad_at_step")
+        self._inject_at = None if inject is None else int(inject)
+        self._current_step: int | None = None  # global step of the running train_step (fit only)
         self._graphed: GraphedStep | None = None
         if bool(cfg.trainer.extra.get("cuda_graph", False)):
             check_graphable(
@@ -426,12 +439,57 @@ class Trainer:
             bucket_sumsq = getattr(self._model, "grad_sumsq", None)
             sq = bucket_sumsq() if bucket_sumsq is not None else None
             norm, coef = fused_clip_coef(self._optimizer.store, max_norm, sumsq=sq)
-            self._optimizer.step(grad_scale=coef)
+            self._optimizer.step(grad_scale=coef)  # skips on device when coef is NaN
         else:
-            norm = torch.nn.utils.clip_grad_norm_(self._model.parameters(), max_norm)
-            self._optimizer.step()
+            norm = torch.nn.utils.clip_grad_norm_(self._model.parameters(), max_norm, error_if_nonfinite=False)
+            if bool(torch.isfinite(norm)):  # module path: one host sync per step decides the skip
+                self._optimizer.step()
+                self._skipped_host[1] = 0
+            else:
+                self._skipped_host[0] += 1
+                self._skipped_host[1] += 1
         self.last_grad_norm = norm  # pre-clip global L2 norm, device scalar (no host sync)
         self._scheduler.step()
+
+    def skipped_steps(self) -> tuple[int, int]:
+        """``(total, consecutive)`` optimizer steps skipped for a non-finite gradient norm (a host
+        read of the fused optimizer's device counters: call it at a sync point)."""
+        dev = getattr(self._optimizer, "skipped", None)
+        if isinstance(dev, torch.Tensor):
+            total, consecutive = (int(v) for v in dev.tolist())
+            return total, consecutive
+        return self._skipped_host[0], self._skipped_host[1]
+
+    def _check_skips(self, step: int) -> int:
+        """Raise once ``max_skipped_steps`` consecutive updates were skipped; returns the total."""
+        total, consecutive = self.skipped_steps()
+        if consecutive >= self._max_skipped:
+            raise FloatingPointError(
+                f"{consecutive} consecutive optimizer steps skipped for a non-finite gradient norm "
+                f"(trainer.extra.max_skipped_steps={self._max_skipped}) at step {step}"
+            )
+        return total
+
+    def _state_finite(self) -> bool:
+        """Weights and optimizer moments all finite (checked before every checkpoint write)."""
+        store = getattr(self._optimizer, "store", None)
+        if store is not None:
+            bufs = [store.master, self._optimizer.exp_avg, self._optimizer.exp_avg_sq]
+        else:
+            bufs = [p.detach() for p in self._raw_model.parameters()]
+            for st in self._optimizer.state.values():
+                bufs += [v for k, v in st.items() if k != "step" and isinstance(v, torch.Tensor)]
+        flags = torch.stack([torch.isfinite(b).all() for b in bufs])
+        return bool(flags.all())
+
+    def _poison_factor(self) -> float:
+        """Fault injection: NaN on the backward seed of the configured step (and rank), else 1."""
+        if self._inject_at is None or self._current_step != self._inject_at:
+            return 1.0
+        target = self._cfg.trainer.extra.get("inject_nonfinite_rank")
+        if target is not None and int(target) != self._rank:
+            return 1.0
+        return float("nan")
 
     def batch_stream(self) -> _Batches:
         """Endless iterator over this trainer's training DataLoader."""
@@ -478,11 +536,15 @@ class Trainer:
         accum = len(dev_batches)
         self._optimizer.zero_grad()
         step_loss = torch.zeros((), dtype=torch.float32, device=self._device)
+        poison = self._poison_factor()
         for micro, batch in enumerate(dev_batches):
             with self._sync_context(micro == accum - 1):
                 with self._policy.autocast():
                     loss, metrics = self._adapter.compute_loss(self._model, batch)
-                (loss / accum).backward()
+                seed = loss / accum
+                if poison != 1.0 and micro == accum - 1:
+                    seed = seed * poison  # gradients only: the logged loss stays finite
+                seed.backward()
             step_loss += _loss_tensor(loss, metrics)
         self._optimizer_step()
         assert self.last_grad_norm is not None
@@ -500,7 +562,7 @@ class Trainer:
             (loss / accum).backward()
             step_loss += _loss_tensor(loss, metrics)
         norm, coef = fused_clip_coef(self._optimizer.store, self._cfg.trainer.max_grad_norm)
-        self._optimizer.step_captured(grad_scale=coef)
+        self._optimizer.step_captured(grad_scale=coef)  # skips on device when coef is NaN
         return step_loss / accum, norm
 
     def _fault_rank(self) -> bool:
@@ -595,7 +657,9 @@ class Trainer:
         for step in range(start_step, max_steps + 1):
             if profiler is not None:
                 profiler.before_step(step)
+            self._current_step = step
             step_loss_dev, step_tokens = self.train_step(batches)
+            self._current_step = None
             if fail_at is not None and step == int(fail_at) and resumed_from_step is None and self._fault_rank():
                 # simulated crash of one incarnation of the job: a resumed run does not re-fire it
                 raise RuntimeError(f"fault injection: trainer.extra.fail_at_step={fail_at} (rank {self._rank})")
@@ -605,8 +669,13 @@ class Trainer:
                 first_step_loss = float(step_loss_dev.item())
 
             if step % cfg.save_every_steps == 0 or step == max_steps:
+                self._check_skips(step)
                 rank_rng = self._gather_rng_states()  # a collective: every rank, every save step
                 if self._ckpt_mgr is not None and self._is_main:
+                    if not self._state_finite():
+                        raise FloatingPointError(
+                            f"refusing to checkpoint step {step}: non-finite weights or optimizer moments"
+                        )
                     extra = {"world_size": self._world_size, "batches_consumed": batches.consumed}
                     if rank_rng is not None:
                         extra["rank_rng_states"] = rank_rng
@@ -624,7 +693,10 @@ class Trainer:
                 lr = float(self._scheduler.get_last_lr()[0])
                 if not math.isfinite(avg_loss) and self._cfg.trainer.extra.get("halt_on_nan", True):
                     raise FloatingPointError(f"non-finite training loss {avg_loss} at step {step}")
-                extra_metrics = self._device_metrics(tps)
+                # logged once a step was skipped (the reference's metric set stays exact otherwise)
+                skipped_total = self._check_skips(step)
+                skip_metric = {"train/skipped_steps": float(skipped_total)} if skipped_total else {}
+                extra_metrics = {**skip_metric, **self._device_metrics(tps)}
                 if self._is_ddp_active:
                     comm_ms = self._exposed_comm_ms()
                     per_rank = self._gather_scalars(
@@ -660,6 +732,7 @@ class Trainer:
                                 "train/tokens_total": float(tokens_global_total),
                                 "train/step_time_sec": step_time,
                                 "train/allreduce_ms": worst_comm_ms,
+                                **skip_metric,
                                 **self._device_metrics(global_tps / self._world_size),
                             },
                             step=step,

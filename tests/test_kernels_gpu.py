@@ -155,6 +155,46 @@ def test_sumsq_and_adamw(gpu_device):
     assert torch.all(shadow[n:] == 0)
 
 
+@pytest.mark.parametrize("offset", [1, 2, 3])
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 1_000_003])
+def test_sumsq_unaligned_views(gpu_device, offset, n):
+    """Bucket views of the flat gradient may start off a 16-byte boundary: the scalar head."""
+    g = torch.Generator(device="cpu").manual_seed(offset * 7 + n)
+    base = torch.randn(n + 8, generator=g).to(gpu_device)
+    x = base[offset : offset + n]
+    assert math.isclose(float(hip().sumsq(x)), float(x.double().pow(2).sum()), rel_tol=1e-5, abs_tol=1e-12)
+
+
+@pytest.mark.parametrize("n", [4096, 1_000_003])  # tiled kernel / grid-stride kernel (ragged)
+def test_adamw_skips_nonfinite_step(gpu_device, n):
+    """A NaN/Inf global norm: clip_coef returns a NaN coefficient and the AdamW kernel writes
+    nothing (weights, moments, shadow unchanged) and counts the skip on device; a finite step then
+    resets the consecutive counter."""
+    g = torch.Generator(device="cpu").manual_seed(9)
+    p = torch.randn(n, generator=g).to(gpu_device)
+    grad = torch.randn(n, generator=g).to(gpu_device)
+    m = (0.1 * torch.randn(n, generator=g)).to(gpu_device)
+    v = torch.rand(n, generator=g).to(gpu_device) * 0.01
+    shadow = p.to(torch.bfloat16)
+    before = [t.clone() for t in (p, m, v, shadow)]
+    skipped = torch.zeros(2, dtype=torch.int32, device=gpu_device)
+    args = (1e-2, 0.9, 0.999, 1e-8, 0.1, 3)
+    for bad in (float("nan"), float("inf")):
+        out = hip().clip_coef(torch.tensor([bad], device=gpu_device), 1.0)
+        assert math.isnan(float(out[1]))
+        hip().adamw_flat(p, grad, m, v, shadow, *args, out[1], None, skipped)
+    assert all(torch.equal(a, b) for a, b in zip((p, m, v, shadow), before))
+    assert skipped.tolist() == [2, 2]
+    out = hip().clip_coef(torch.tensor([16.0], device=gpu_device), 1.0)
+    assert torch.equal(out.cpu(), ref.clip_coef(torch.tensor(16.0), 1.0))
+    hip().adamw_flat(p, grad, m, v, shadow, *args, out[1], None, skipped)
+    p_r, m_r, v_r = before[0].clone(), before[1].clone(), before[2].clone()
+    ref.adamw_flat(p_r, grad, m_r, v_r, None, lr=1e-2, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.1, step=3,
+                   grad_scale=out[1])
+    _close(p, p_r, 1e-6, 1e-5, "param after the applied step")
+    assert skipped.tolist() == [2, 0]
+
+
 def test_adamw_matches_torch_adamw(gpu_device):
     """Several steps of the fused kernel track torch.optim.AdamW (the reference optimizer)."""
     g = torch.Generator(device="cpu").manual_seed(8)

@@ -513,9 +513,12 @@ void wgrad_gemm_pp(const Tensor& dy, const Tensor& x, Tensor c, const c10::optio
 // ---- fused forward / dX GEMM ------------------------------------------------------------------
 // out = epi(a @ op(b)): b is [N, K] (weight, forward) or, with b_kn, [K, N] (weight in dX = dy @ W).
 // epilogue 0 -> (out, None); 1 -> (u, gelu(u)); 2 -> (du = acc * gelu'(u), None) with dbias += colsum.
+// `out_opt` (epilogue 0): write C into this [M, N] bf16 tensor (e.g. a row chunk of a larger output)
+// instead of a fresh allocation — no copy of a multi-GB result.
 std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tensor& b, bool b_kn, int64_t epilogue,
                                                      const c10::optional<Tensor>& bias, const c10::optional<Tensor>& u,
-                                                     c10::optional<Tensor> dbias, int64_t seq_len) {
+                                                     c10::optional<Tensor> dbias, int64_t seq_len,
+                                                     const c10::optional<Tensor>& out_opt) {
   check_gpu(a, "a");
   check_gpu(b, "b");
   check_dtype(a, at::kBFloat16, "a");
@@ -546,7 +549,18 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tens
   g.N = (int)N;
   g.K = (int)K;
   g.epilogue = (int)epilogue;
-  Tensor out = at::empty({M, N}, a.options());
+  Tensor out;
+  if (out_opt.has_value()) {
+    TORCH_CHECK(epilogue == 0, "gemm_fused: out= is for epilogue 0");
+    check_gpu(*out_opt, "out");
+    check_dtype(*out_opt, at::kBFloat16, "out");
+    TORCH_CHECK(out_opt->dim() == 2 && out_opt->size(0) == M && out_opt->size(1) == N && out_opt->is_contiguous(),
+                "gemm_fused: out must be a contiguous [M, N] tensor");
+    TORCH_CHECK((uintptr_t)out_opt->data_ptr() % 16 == 0, "gemm_fused: out must be 16-byte aligned");
+    out = *out_opt;
+  } else {
+    out = at::empty({M, N}, a.options());
+  }
   c10::optional<Tensor> out2;
   g.c = out.data_ptr();
   g.ldc = (int)N;
@@ -711,7 +725,7 @@ TORCH_LIBRARY(llmtrain_hip, m) {
   m.def("set_dropout_seed_offset(Tensor? word) -> ()", &set_dropout_seed_offset);
   m.def("wgrad_gemm_pp(Tensor dy, Tensor x, Tensor(a!) c, Tensor(b!)? bias=None, int split=0, int mode=-1) -> ()");
   m.def("gemm_fused(Tensor a, Tensor b, bool b_kn, int epilogue, Tensor? bias=None, Tensor? u=None,"
-        " Tensor(a!)? dbias=None, int seq_len=0) -> (Tensor, Tensor?)");
+        " Tensor(a!)? dbias=None, int seq_len=0, Tensor(b!)? out=None) -> (Tensor, Tensor?)");
   m.def("sumsq(Tensor x) -> Tensor");
   m.def("adamw_flat(Tensor(a!) param, Tensor grad, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor(d!)? shadow,"
         " float lr, float beta1, float beta2, float eps, float weight_decay, int step, Tensor? grad_scale,"

@@ -62,15 +62,16 @@ def _on_gpu(t: torch.Tensor) -> bool:
 _POLICY = {"gemm_all_ours": False, "single_stream": False, "deterministic": False}
 
 # How run.deterministic keeps the step bitwise reproducible (LLMTRAIN_DET_SCHEDULE overrides):
-#  * "serial": the weight-gradient GEMMs run on the main stream (no side stream), the forward / dX
-#    GEMMs stay on hipBLASLt's tuned solutions except the LM-head dX (our kernel: the one library
-#    GEMM measured non-reproducible in this schedule, docs/round4.md section 3).  Evidence for the
-#    library GEMMs that remain: bitwise-equal repeats at micro-batch 8 and 32 of GPT-2 124M and
-#    at micro-batch 32 of GPT-2 XL (the XL preset; 3 whole runs x 20 steps) (bench/determinism_probe.py,
-#    profiles/r4/det/, profiles/r5/det/) and 800 bitwise repeats of the
-#    Stream-K solutions of the LM-head logits and forward projections, alone and beside a
-#    concurrent stream (bench/sk_repeat.py); other shapes are unpinned, and each library GEMM of a
-#    serial run is named once in the log (_det_library).
+#  * "serial": the weight-gradient GEMMs run on the main stream (no side stream), the LM-head logits
+#    and dX GEMMs on our fixed-order kernel (the logits' tuned library solution is a Stream-K kernel
+#    and the one library GEMM of the configuration whose bitwise guarantee failed once,
+#    profiles/r5/det/; round 6 took it off the library), and the other forward / dX GEMMs on our
+#    kernel below the size cap, on hipBLASLt's tuned solutions above it.  Evidence for the library
+#    GEMMs that remain: bitwise-equal repeats at micro-batch 32 of GPT-2 124M and GPT-2 XL (the
+#    XL preset; 3 whole runs x 20 steps) (bench/determinism_probe.py, profiles/r4/det/,
+#    profiles/r5/det/) and 800 bitwise repeats of the Stream-K solutions of the forward
+#    projections, alone and beside a concurrent stream (bench/sk_repeat.py); other shapes are
+#    unpinned, and each library GEMM of a serial run is named once in the log (_det_library).
 #  * "ours": every forward / dX GEMM on the hand-written kernel (csrc/gemm_fused.hip), side stream
 #    kept; slower because that kernel trails hipBLASLt at 128K rows (docs/round4.md).
 DET_SCHEDULES = ("serial", "ours")
@@ -373,6 +374,17 @@ def _fgemm_ok(a: torch.Tensor, k: int, n: int, *others: torch.Tensor | None, op:
     return True
 
 
+def _fgemm_ok_any_size(a: torch.Tensor, k: int, n: int, *others: torch.Tensor | None, op: str = "") -> bool:
+    """:func:`_fgemm_ok` without the A-size routing cap (row-chunked callers: the LM head)."""
+    if not (k % 64 == 0 and k >= 256 and n % 8 == 0):
+        _det_fallback(f"GEMM {op or 'linear'} K={k} N={n} (needs K % 64 == 0, K >= 256, N % 8 == 0)", always=True)
+        return False
+    if not all(t is None or t.data_ptr() % 16 == 0 for t in (a, *others)) or a.stride(1) != 1:
+        _det_fallback(f"GEMM {op or 'linear'} with an operand not 16-byte aligned", always=True)
+        return False
+    return True
+
+
 # The hand-written GEMM's buffer descriptors and tile offsets are 32-bit byte offsets: every [M, K]
 # operand and [M, N] output must stay below 2 GiB (the binding refuses larger ones).  Larger GEMMs run
 # as row chunks (GPT-2 124M at micro-batch >= ~342, XL's d_ff = 6400 past ~168K rows), each chunk a
@@ -459,14 +471,19 @@ _HEAD_ROWS = 16384
 
 
 def head_logits(h, w):
-    """``logits = h @ w^T`` for the vocab-padded LM head ``w [Vp, d]``: hipBLASLt, or row chunks
-    of the hand-written GEMM when every GEMM runs on our kernels (deterministic "ours" schedule)."""
-    if not (_on_gpu(h) and _POLICY["gemm_all_ours"] and h.dtype == torch.bfloat16 and _fgemm_ok(h, h.shape[1], w.shape[0], w)):
+    """``logits = h @ w^T`` for the vocab-padded LM head ``w [Vp, d]``: hipBLASLt on the fast path;
+    in deterministic mode (either schedule) row chunks of the hand-written fixed-order kernel,
+    written in place into one ``[M, Vp]`` output.  The library's tuned solution for this shape is a
+    Stream-K kernel (``SK3``), which combines partial tiles in completion order — the one library
+    GEMM left in the serial schedule when its bitwise guarantee failed once
+    (profiles/r5/det/pytest_gpu_serial_divergence.txt, docs/round6.md §2)."""
+    if not (_on_gpu(h) and _POLICY["deterministic"] and h.dtype == torch.bfloat16
+            and _fgemm_ok_any_size(h, h.shape[1], w.shape[0], w, op="LM-head logits")):
         return _lib_mm(h, w.t(), op="LM-head logits")
     out = torch.empty(h.shape[0], w.shape[0], dtype=h.dtype, device=h.device)
     for r0 in range(0, h.shape[0], _HEAD_ROWS):
         r1 = min(h.shape[0], r0 + _HEAD_ROWS)
-        out[r0:r1] = hip_ops().gemm_fused(h[r0:r1], w, False, 0, None)[0]
+        hip_ops().gemm_fused(h[r0:r1], w, False, 0, None, None, None, 0, out[r0:r1])
     return out
 
 
@@ -487,7 +504,7 @@ def head_dx(dlogits, w):
     out = torch.empty(dlogits.shape[0], w.shape[1], dtype=dlogits.dtype, device=dlogits.device)
     for r0 in range(0, dlogits.shape[0], _HEAD_ROWS):
         r1 = min(dlogits.shape[0], r0 + _HEAD_ROWS)
-        out[r0:r1] = hip_ops().gemm_fused(dlogits[r0:r1], w, True, 0)[0]
+        hip_ops().gemm_fused(dlogits[r0:r1], w, True, 0, None, None, None, 0, out[r0:r1])
     return out
 
 

@@ -1,6 +1,7 @@
 """Build the in-tree HIP extension ``llmtrain/ops/_llmtrain_hip.so`` for gfx950.
 
     python -m llmtrain.ops.build [--jobs N] [--force] [--debug]
+    python -m llmtrain.ops.build --variant NAME -D MACRO[=VALUE] ...   # A/B build of the same sources
 
 Every ``csrc/*.hip`` kernel file is compiled by ``hipcc --offload-arch=gfx950`` into its own
 object (these TUs include only the HIP runtime, so they compile in seconds); ``csrc/bindings.cpp``
@@ -32,6 +33,10 @@ OUT = Path(__file__).resolve().with_name("_llmtrain_hip.so")
 # of the release object when LLMTRAIN_DEBUG_KERNELS=1 (see llmtrain/ops/_ext.py)
 OUT_DEBUG = Path(__file__).resolve().with_name("_llmtrain_hip_debug.so")
 OBJDIR = REPO / "build" / "hip_obj"
+# `--variant NAME -D ...`: the same sources with extra preprocessor defines, linked to
+# llmtrain/ops/variants/_llmtrain_hip_NAME.so (in-tree, so it travels to the GPU box) and loaded in
+# place of the release object through LLMTRAIN_HIP_EXT — same-box A/B of a kernel change
+VARIANTS = Path(__file__).resolve().with_name("variants")
 ARCH = "gfx950"  # MI355X (CDNA4) only
 
 
@@ -83,11 +88,11 @@ def _stale(obj: Path, src: Path) -> bool:
     return any(p.stat().st_mtime > mtime for p in [src, *_headers(), Path(__file__)])
 
 
-def _compile(src: Path, debug: bool, force: bool) -> Path:
-    obj = OBJDIR / (src.name + (".dbg" if debug else "") + ".o")
+def _compile(src: Path, debug: bool, force: bool, objdir: Path = OBJDIR, defines: tuple[str, ...] = ()) -> Path:
+    obj = objdir / (src.name + (".dbg" if debug else "") + ".o")
     if not force and not _stale(obj, src):
         return obj
-    cmd = [_hipcc(), *_common_flags(debug)]
+    cmd = [_hipcc(), *_common_flags(debug), *(f"-D{d}" for d in defines)]
     if src.suffix == ".cpp":
         cmd += ["-x", "hip", *_torch_flags()]
     cmd += ["-c", str(src), "-o", str(obj)]
@@ -97,15 +102,22 @@ def _compile(src: Path, debug: bool, force: bool) -> Path:
     return obj
 
 
-def build(*, jobs: int | None = None, force: bool = False, debug: bool = False, verbose: bool = True) -> Path:
+def build(
+    *, jobs: int | None = None, force: bool = False, debug: bool = False, verbose: bool = True,
+    variant: str | None = None, defines: tuple[str, ...] = (),
+) -> Path:
     """Compile every kernel for gfx950 and link the extension; returns the .so path."""
-    OBJDIR.mkdir(parents=True, exist_ok=True)
+    objdir = OBJDIR if variant is None else OBJDIR.parent / f"hip_obj_{variant}"
+    objdir.mkdir(parents=True, exist_ok=True)
     sources = sorted(CSRC.glob("*.hip")) + [CSRC / "bindings.cpp"]
     jobs = jobs or min(16, os.cpu_count() or 4, len(sources))
     with ThreadPoolExecutor(max_workers=jobs) as pool:
-        objs = list(pool.map(lambda s: _compile(s, debug, force), sources))
+        objs = list(pool.map(lambda s: _compile(s, debug, force, objdir, defines), sources))
     newest = max(o.stat().st_mtime for o in objs)
     out = OUT_DEBUG if debug else OUT
+    if variant is not None:
+        VARIANTS.mkdir(exist_ok=True)
+        out = VARIANTS / f"_llmtrain_hip_{variant}.so"
     if force or not out.exists() or out.stat().st_mtime < newest:
         _, lib = _torch_dirs()
         cmd = [
@@ -128,8 +140,13 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--variant", default=None, help="A/B build name (llmtrain/ops/variants/)")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="extra define for --variant")
     args = ap.parse_args(argv)
-    build(jobs=args.jobs, force=args.force, debug=args.debug)
+    if args.defines and args.variant is None:
+        ap.error("-D needs --variant (the release build takes no extra defines)")
+    build(jobs=args.jobs, force=args.force or bool(args.defines), debug=args.debug, variant=args.variant,
+          defines=tuple(args.defines))
     return 0
 
 

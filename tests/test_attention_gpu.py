@@ -149,22 +149,40 @@ def test_padding_does_not_change_valid_rows(gpu_device) -> None:
 @pytest.mark.parametrize("hd,B,T,H", [(64, 2, 200, 3), (128, 2, 200, 3), (64, 64, 300, 4)])
 def test_attention_dropout_head_dims(gpu_device, hd: int, B: int, T: int, H: int) -> None:
     """Probability dropout at head dims 64 and 128 (and, B*H = 256, the per-(b, h) backward grid)
-    against the counter-based torch reference (``ops/reference.py``: the same keep mask, the
-    undropped normaliser in lse)."""
+    against fp32 AUTOGRAD of eager dropout attention (reference ``models/gpt.py:56-69`` with
+    ``attn_dropout`` on the probabilities).  Only the keep mask is shared with the kernel — the
+    counter hash of ``ops/reference.attn_dropout_keep``, which any correct implementation must
+    reproduce bit for bit; the oracle forms its own softmax, lse, O and gradients from the bf16
+    inputs, so no kernel output (O, lse) feeds it."""
     from llmtrain.ops import reference as ref
 
     g = torch.Generator(device="cpu").manual_seed(hd)
     qkv = torch.randn(B * T, 3 * hd * H, generator=g).to(torch.bfloat16)
     dout = torch.randn(B * T, hd * H, generator=g).to(torch.bfloat16)
-    adrop = (0.25, ref.dropout_site_seed(11, 8))
-    out_g, lse_g = ops.attn_fwd(qkv.to(gpu_device), B, T, H, dropout=adrop)
-    out_r, lse_r = ref.attn_fwd(qkv, B, T, H, *adrop)
-    torch.testing.assert_close(lse_g.cpu(), lse_r, atol=2e-3, rtol=2e-3)
-    torch.testing.assert_close(out_g.cpu().float(), out_r.float(), atol=3e-2, rtol=3e-2)
+    p_drop, seed = 0.25, ref.dropout_site_seed(11, 8)
+    out_g, lse_g = ops.attn_fwd(qkv.to(gpu_device), B, T, H, dropout=(p_drop, seed))
     dbias = torch.zeros(3 * hd * H, device=gpu_device)
-    dq_g = ops.attn_bwd(dout.to(gpu_device), qkv.to(gpu_device), out_g, lse_g, B, T, H, dropout=adrop,
+    dq_g = ops.attn_bwd(dout.to(gpu_device), qkv.to(gpu_device), out_g, lse_g, B, T, H, dropout=(p_drop, seed),
                         qkv_bias_grad=dbias).cpu().float()
-    dq_r = ref.attn_bwd(dout, qkv, out_g.cpu(), lse_g.cpu(), B, T, H, *adrop).float()
-    assert (dq_g - dq_r).abs().max().item() < 2e-2 * dq_r.abs().max().item()
+
+    # independent oracle: fp32 eager attention with the mask applied to the probabilities
+    keep = ref.attn_dropout_keep(seed, p_drop, B, H, T, torch.device("cpu"))  # [B, H, T, T]
+    x = qkv.float().detach().requires_grad_(True)
+    q, k, v = (t.transpose(1, 2) for t in x.view(B, T, 3, H, hd).unbind(dim=2))
+    s = (q @ k.transpose(-2, -1)) / math.sqrt(hd)
+    causal = torch.ones(T, T, dtype=torch.bool).triu(1)[None, None]
+    s = s.masked_fill(causal, torch.finfo(torch.float32).min)
+    lse_r = torch.logsumexp(s, dim=-1)  # the undropped normaliser the kernel stores
+    _, dscale = ref.dropout_params(p_drop)  # 1 / keep probability of the 16-bit threshold
+    probs = torch.where(keep, torch.softmax(s, dim=-1) * dscale, torch.zeros(()))
+    out_r = (probs @ v).transpose(1, 2).reshape(B * T, H * hd)
+    out_r.backward(dout.float())
+    dq_r = x.grad
+
+    torch.testing.assert_close(lse_g.cpu(), lse_r, atol=2e-3, rtol=2e-3)
+    _check("out (dropout)", out_g.cpu(), out_r.detach(), hd)
+    a, r = dq_g.view(B * T, 3, H, hd), dq_r.view(B * T, 3, H, hd)
+    for i, name in enumerate(("dq", "dk", "dv")):
+        _check(f"{name} (dropout)", a[:, i], r[:, i], hd)
     want = dq_r.sum(dim=0)
     assert (dbias.cpu() - want).abs().max().item() < 2e-2 * want.abs().max().item()

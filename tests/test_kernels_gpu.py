@@ -347,6 +347,12 @@ def test_gemm_fused_bias(gpu_device, M, N, K, b_kn):
     _close(out_nb, a.float() @ w.float().t(), 2e-2, 1e-2, "gemm")
     again, _ = hip().gemm_fused(a, b, b_kn, 0, bias)
     assert torch.equal(out, again), "gemm_fused is not deterministic (pipeline race?)"
+    # out=: written in place into a row slice of a larger tensor, rows around it untouched
+    big = torch.full((M + 16, N), 7.0, device=gpu_device, dtype=torch.bfloat16)
+    ret, _ = hip().gemm_fused(a, b, b_kn, 0, bias, None, None, 0, big[8 : 8 + M])
+    assert ret.data_ptr() == big[8].data_ptr()
+    assert torch.equal(big[8 : 8 + M], out)
+    assert torch.all(big[:8] == 7.0) and torch.all(big[8 + M :] == 7.0)
 
 
 @pytest.mark.parametrize("M,N,K", GEMM_SHAPES)

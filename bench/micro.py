@@ -216,7 +216,7 @@ def ln(M: int = 65536, d: int = 768) -> None:
     print(json.dumps({"op": "gelu_fwd", "ms": round(ms, 4), "GB/s": round(gb / ms * 1e3, 1)}), flush=True)
 
 
-def attn(B: int = 32, T: int = 1024, H: int = 12) -> list[dict]:
+def attn(B: int = 32, T: int = 1024, H: int = 12, sdpa: bool = True) -> list[dict]:
     from llmtrain.ops import _ext
 
     _ext.require()
@@ -237,6 +237,10 @@ def attn(B: int = 32, T: int = 1024, H: int = 12) -> list[dict]:
     ms = timeit(lambda: ops.attn_bwd(dout, qkv, out, lse, B, T, H, 0.0, 0, None, delta))
     rows.append({"attn": "llmtrain bwd, delta ready", "ms": round(ms, 4),
                  "TFLOPs": round(2.5 * flops_fwd / ms / 1e9, 1)})
+    if not sdpa:
+        for r in rows:
+            print(json.dumps({"B": B, "H": H, **r}), flush=True)
+        return rows
     q, k, v = (t.transpose(1, 2).contiguous() for t in qkv.view(B, T, 3, H, 64).unbind(2))
     q.requires_grad_(True); k.requires_grad_(True); v.requires_grad_(True)
     do = dout.view(B, T, H, 64).transpose(1, 2).contiguous()
@@ -274,5 +278,7 @@ if __name__ == "__main__":
         fgemm(int(sys.argv[2]) if len(sys.argv) > 2 else 16384, only="xl")
     if what == "fgemm_head":  # LM-head shapes (K 768 fwd, K 50304 dX)
         fgemm(int(sys.argv[2]) if len(sys.argv) > 2 else 32768, only="head")
+    if what == "attn_ours":  # B H: our kernels only (A/B of builds via LLMTRAIN_HIP_EXT)
+        attn(int(sys.argv[2]), 1024, int(sys.argv[3]), sdpa=False)
     if what in ("attn", "all"):
         attn(int(sys.argv[2]) if what == "attn" and len(sys.argv) > 2 else 32)

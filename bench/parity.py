@@ -11,7 +11,9 @@ optimizer/schedule, then reports the full-val-split loss.  Paths:
 * ``fused``       — llmtrain engine: hand-written gfx950 kernels, bf16 compute, fp32 master weights;
 * ``module_bf16`` — the torch nn.Module path under bf16 autocast (SDPA attention, torch AdamW);
 * ``module_fp32`` — the torch nn.Module path in fp32: the reference's numerics (gpt.py:35-76,
-                    trainer.py:93-97 AdamW, :390-393 clip) — the parity oracle.
+                    trainer.py:93-97 AdamW, :390-393 clip) — the parity oracle;
+* ``fused:bf16_grad`` / ``fused:bf16`` — the engine with the residual-gradient stream (or the residual
+                    stream and its gradient) stored in bf16 (``model.extra.residual_dtype``).
 
 One JSON line per path plus a summary line with the relative val-loss gaps.  The default schedule
 (lr 3e-4, warm-up over the first third, 32 x 1024-token sequences per step) keeps GPT-2 124M out of
@@ -47,8 +49,10 @@ def run_path(path: str, args: argparse.Namespace) -> dict:
     from llmtrain.training.trainer import Trainer
 
     model = dict(MODELS[args.model], name="gpt", dropout=args.dropout, tie_embeddings=True)
-    fused = path == "fused"
+    fused = path.split(":")[0] == "fused"
     model["extra"] = {"fused": fused}
+    if fused and ":" in path:
+        model["extra"]["residual_dtype"] = path.split(":", 1)[1]
     precision = "fp32" if path == "module_fp32" else "bf16"
     if args.device == "cpu":
         precision = "fp32"

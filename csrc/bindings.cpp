@@ -70,7 +70,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> add_layernorm_fwd(const Tensor& x, co
                                                              at::ScalarType out_dtype, double dropout_p,
                                                              int64_t dropout_seed) {
   check_gpu(x, "x");
-  check_dtype(x, at::kFloat, "x");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x must be f32 or bf16");
   check_gpu(w, "weight");
   check_gpu(b, "bias");
   check_dtype(w, at::kFloat, "weight");
@@ -89,14 +89,15 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> add_layernorm_fwd(const Tensor& x, co
     a.delta = delta->data_ptr();
     a.delta_bf16 = is_lowp(*delta, "delta");
     xs = at::empty_like(x);
-    a.xs_out = xs.data_ptr<float>();
+    a.xs_out = xs.data_ptr();
   } else {
     xs = at::empty({0}, x.options());
   }
   Tensor y = at::empty({M, d}, x.options().dtype(out_dtype));
-  Tensor mean = at::empty({M}, x.options());
-  Tensor rstd = at::empty({M}, x.options());
-  a.x = x.data_ptr<float>();
+  Tensor mean = at::empty({M}, x.options().dtype(at::kFloat));
+  Tensor rstd = at::empty({M}, x.options().dtype(at::kFloat));
+  a.x = x.data_ptr();
+  a.x_bf16 = x.scalar_type() == at::kBFloat16;
   a.w = w.data_ptr<float>();
   a.b = b.data_ptr<float>();
   a.y = y.data_ptr();
@@ -116,10 +117,10 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_impl(const Tensor& dy, const Te
                                                       const c10::optional<Tensor>& dresid, Tensor dw, Tensor db,
                                                       const c10::optional<Tensor>& dy_scale, bool want_lowp,
                                                       const c10::optional<Tensor>& dproj, double dropout_p,
-                                                      int64_t dropout_seed, bool defer_params) {
+                                                      int64_t dropout_seed, bool defer_params, bool grad_lowp) {
   check_gpu(dy, "dy");
   check_gpu(xs, "xs");
-  check_dtype(xs, at::kFloat, "xs");
+  TORCH_CHECK(xs.scalar_type() == at::kFloat || xs.scalar_type() == at::kBFloat16, "xs must be f32 or bf16");
   TORCH_CHECK(dy.sizes() == xs.sizes() && xs.dim() == 2, "dy/xs must be [M, d]");
   const int64_t M = xs.size(0), d = xs.size(1);
   TORCH_CHECK(d % 4 == 0 && d <= 2048, "LayerNorm kernel needs d % 4 == 0 and d <= 2048");
@@ -137,15 +138,20 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_impl(const Tensor& dy, const Te
   llmt::LnBwdArgs a{};
   a.dy = dy.data_ptr();
   a.dy_bf16 = is_lowp(dy, "dy");
-  a.xs = xs.data_ptr<float>();
+  a.xs = xs.data_ptr();
+  a.xs_bf16 = xs.scalar_type() == at::kBFloat16;
+  a.grad_bf16 = grad_lowp;
+  TORCH_CHECK(a.dy_bf16 || !(a.xs_bf16 || grad_lowp), "layernorm_bwd: bf16 residual / gradient stream needs bf16 dy");
+  TORCH_CHECK(grad_lowp || !a.xs_bf16, "layernorm_bwd: a bf16 residual stream takes a bf16 gradient stream");
+  const auto gdt = grad_lowp ? at::kBFloat16 : at::kFloat;
   a.mean = mean.data_ptr<float>();
   a.rstd = rstd.data_ptr<float>();
   a.w = w.data_ptr<float>();
   if (dresid.has_value()) {
     check_gpu(*dresid, "dresid");
-    check_dtype(*dresid, at::kFloat, "dresid");
+    check_dtype(*dresid, gdt, "dresid (the gradient stream's dtype)");
     TORCH_CHECK(dresid->sizes() == xs.sizes(), "dresid must match xs");
-    a.dresid = dresid->data_ptr<float>();
+    a.dresid = dresid->data_ptr();
   }
   if (dy_scale.has_value()) {
     check_gpu(*dy_scale, "dy_scale");
@@ -153,10 +159,12 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_impl(const Tensor& dy, const Te
     TORCH_CHECK(dy_scale->numel() == 1, "dy_scale must be a scalar");
     a.dy_scale = dy_scale->data_ptr<float>();
   }
-  Tensor dx = at::empty_like(xs);
-  Tensor dx_lp = want_lowp ? at::empty_like(dy) : at::empty({0}, dy.options());
-  a.dx = dx.data_ptr<float>();
-  a.dx_lp = want_lowp ? dx_lp.data_ptr() : nullptr;
+  Tensor dx = at::empty(xs.sizes(), xs.options().dtype(gdt));
+  // a bf16 gradient stream without branch dropout IS the bf16 GEMM operand: no second write
+  const bool lp_is_dx = want_lowp && grad_lowp && dropout_p <= 0.0;
+  Tensor dx_lp = want_lowp ? (lp_is_dx ? dx : at::empty_like(dy)) : at::empty({0}, dy.options());
+  a.dx = dx.data_ptr();
+  a.dx_lp = want_lowp && !lp_is_dx ? dx_lp.data_ptr() : nullptr;
   a.dw = dw.data_ptr<float>();
   a.db = db.data_ptr<float>();
   if (dproj.has_value()) {
@@ -170,9 +178,9 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_impl(const Tensor& dy, const Te
   a.dropout = make_dropout(dropout_p, dropout_seed);
   a.defer_params = defer_params;
   TORCH_CHECK(!(defer_params && a.dproj != nullptr), "layernorm_bwd: deferred reduce takes no dproj_bias");
-  Tensor parts = at::empty({0}, xs.options());
+  Tensor parts = at::empty({0}, xs.options().dtype(at::kFloat));
   if (M > 0) {
-    Tensor ws = workspace(xs, llmt::layernorm_bwd_ws_floats(a));
+    Tensor ws = workspace(mean, llmt::layernorm_bwd_ws_floats(a));
     a.ws = ws.data_ptr<float>();
     check_hip(llmt::launch_layernorm_bwd(a, cur_stream()), "layernorm_bwd");
     // [2 (dw, db), grid, d] partial rows at the front of the workspace
@@ -184,9 +192,10 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_impl(const Tensor& dy, const Te
 std::tuple<Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor& xs, const Tensor& mean, const Tensor& rstd,
                                          const Tensor& w, const c10::optional<Tensor>& dresid, Tensor dw, Tensor db,
                                          const c10::optional<Tensor>& dy_scale, bool want_lowp,
-                                         const c10::optional<Tensor>& dproj, double dropout_p, int64_t dropout_seed) {
+                                         const c10::optional<Tensor>& dproj, double dropout_p, int64_t dropout_seed,
+                                         bool grad_lowp) {
   auto r = layernorm_bwd_impl(dy, xs, mean, rstd, w, dresid, dw, db, dy_scale, want_lowp, dproj, dropout_p,
-                              dropout_seed, false);
+                              dropout_seed, false, grad_lowp);
   return {std::get<0>(r), std::get<1>(r)};
 }
 
@@ -196,9 +205,9 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd_deferred(const Tensor& dy, cons
                                                           const Tensor& rstd, const Tensor& w,
                                                           const c10::optional<Tensor>& dresid, Tensor dw, Tensor db,
                                                           const c10::optional<Tensor>& dy_scale, bool want_lowp,
-                                                          double dropout_p, int64_t dropout_seed) {
+                                                          double dropout_p, int64_t dropout_seed, bool grad_lowp) {
   return layernorm_bwd_impl(dy, xs, mean, rstd, w, dresid, dw, db, dy_scale, want_lowp, c10::nullopt, dropout_p,
-                            dropout_seed, true);
+                            dropout_seed, true, grad_lowp);
 }
 
 // dst[j] += sum over rows of parts[j // 2][j % 2] for every deferred LayerNorm: ONE launch for up to
@@ -312,7 +321,8 @@ void colsum_accum(const Tensor& dy, Tensor out) {
   }
 }
 
-Tensor embedding_fwd(const Tensor& ids, const Tensor& wte, const Tensor& wpe, double dropout_p, int64_t dropout_seed) {
+Tensor embedding_fwd(const Tensor& ids, const Tensor& wte, const Tensor& wpe, double dropout_p, int64_t dropout_seed,
+                     bool out_lowp) {
   check_gpu(ids, "ids");
   check_gpu(wte, "wte");
   check_gpu(wpe, "wpe");
@@ -323,10 +333,10 @@ Tensor embedding_fwd(const Tensor& ids, const Tensor& wte, const Tensor& wpe, do
   const int64_t B = ids.size(0), T = ids.size(1), d = wte.size(1);
   TORCH_CHECK(wpe.size(1) == d && wpe.size(0) >= T && d % 4 == 0, "embedding shapes");
   at::hip::HIPGuardMasqueradingAsCUDA guard(ids.device());
-  Tensor x = at::empty({B * T, d}, wte.options());
+  Tensor x = at::empty({B * T, d}, wte.options().dtype(out_lowp ? at::kBFloat16 : at::kFloat));
   if (B * T > 0)
     check_hip(llmt::launch_embedding_fwd(ids.data_ptr<int64_t>(), wte.data_ptr<float>(), wpe.data_ptr<float>(),
-                                         x.data_ptr<float>(), (int)B, (int)T, (int)d, (int)wte.size(0),
+                                         x.data_ptr(), out_lowp, (int)B, (int)T, (int)d, (int)wte.size(0),
                                          make_dropout(dropout_p, dropout_seed), cur_stream()),
               "embedding_fwd");
   return x;
@@ -702,17 +712,18 @@ TORCH_LIBRARY(llmtrain_hip, m) {
         " float dropout_p=0., int dropout_seed=0) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("layernorm_bwd(Tensor dy, Tensor xs, Tensor mean, Tensor rstd, Tensor weight, Tensor? dresid,"
         " Tensor(a!) dweight, Tensor(b!) dbias, Tensor? dy_scale, bool want_lowp, Tensor(c!)? dproj_bias,"
-        " float dropout_p=0., int dropout_seed=0) -> (Tensor, Tensor)");
+        " float dropout_p=0., int dropout_seed=0, bool grad_lowp=False) -> (Tensor, Tensor)");
   m.def("layernorm_bwd_deferred(Tensor dy, Tensor xs, Tensor mean, Tensor rstd, Tensor weight, Tensor? dresid,"
         " Tensor(a!) dweight, Tensor(b!) dbias, Tensor? dy_scale, bool want_lowp, float dropout_p=0.,"
-        " int dropout_seed=0) -> (Tensor, Tensor, Tensor)");
+        " int dropout_seed=0, bool grad_lowp=False) -> (Tensor, Tensor, Tensor)");
   m.def("ln_param_reduce(Tensor[] parts, Tensor(a!)[] dst) -> ()");
   m.def("cross_entropy_fwd_bwd(Tensor(a!) logits, Tensor labels, int vocab, Tensor row_weight) -> Tensor");
   m.def("gelu_fwd(Tensor u) -> Tensor");
   m.def("scale(Tensor x, Tensor s) -> Tensor");
   m.def("gelu_bwd(Tensor dg, Tensor u, Tensor(a!)? dbias) -> Tensor");
   m.def("colsum_accum(Tensor dy, Tensor(a!) out) -> ()");
-  m.def("embedding_fwd(Tensor ids, Tensor wte, Tensor wpe, float dropout_p=0., int dropout_seed=0) -> Tensor");
+  m.def("embedding_fwd(Tensor ids, Tensor wte, Tensor wpe, float dropout_p=0., int dropout_seed=0,"
+        " bool out_lowp=False) -> Tensor");
   m.def("embedding_bwd(Tensor dx, Tensor ids, Tensor(a!) dwte, Tensor(b!) dwpe, float dropout_p=0.,"
         " int dropout_seed=0) -> ()");
   m.def("attn_fwd(Tensor qkv, int B, int T, int H, float dropout_p=0., int dropout_seed=0,"

@@ -173,11 +173,13 @@ __global__ __launch_bounds__(256) void colwise_kernel(const void* __restrict__ a
   }
 }
 
-// one wave per token row; float4 chunks
+// one wave per token row; float4 chunks; OUT_BF16: the residual stream starts in bf16 (the engine's
+// bf16 residual option), the sum and the dropout scale stay fp32 in registers
+template <bool OUT_BF16>
 __global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __restrict__ ids,
                                                             const float* __restrict__ wte,
                                                             const float* __restrict__ wpe,
-                                                            float* __restrict__ x, int M, int T,
+                                                            void* __restrict__ x, int M, int T,
                                                             int d, int V, DropoutArgs dr) {
   resolve_dropout(dr);
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -189,7 +191,6 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __res
   const int t = (int)(row % T);
   const float4_t* e = reinterpret_cast<const float4_t*>(wte + tok * (long)d);
   const float4_t* p = reinterpret_cast<const float4_t*>(wpe + (long)t * d);
-  float4_t* o = reinterpret_cast<float4_t*>(x + row * (long)d);
   for (int c = lane; c < (d >> 2); c += 64) {
     float4_t v = e[c] + p[c];
     if (dr.thr != 0) {  // embedding dropout (reference gpt.py:179 self.drop)
@@ -197,7 +198,13 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __res
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[k] = drop_keep(dr.seed, dr.thr, e0 + k) ? v[k] * dr.scale : 0.f;
     }
-    o[c] = v;
+    if (OUT_BF16) {
+      ushort4_t ov;
+      ov[0] = f2bf(v[0]); ov[1] = f2bf(v[1]); ov[2] = f2bf(v[2]); ov[3] = f2bf(v[3]);
+      reinterpret_cast<ushort4_t*>(static_cast<bf16_raw*>(x) + row * (long)d)[c] = ov;
+    } else {
+      reinterpret_cast<float4_t*>(static_cast<float*>(x) + row * (long)d)[c] = v;
+    }
   }
 }
 
@@ -310,12 +317,16 @@ hipError_t launch_colsum_accum(const void* dy, bool bf16, float* out, float* ws,
   return launch_colsum_reduce(ws, (int)grid.y, N, out, ws + (long)grid.y * N, stream);
 }
 
-hipError_t launch_embedding_fwd(const int64_t* ids, const float* wte, const float* wpe, float* x, int B,
+hipError_t launch_embedding_fwd(const int64_t* ids, const float* wte, const float* wpe, void* x, bool x_bf16, int B,
                                 int T, int d, int V, DropoutArgs dropout, hipStream_t stream) {
   if (d % 4 != 0) return hipErrorInvalidValue;
   const int M = B * T;
-  hipLaunchKernelGGL(embedding_fwd_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, ids, wte, wpe, x, M, T, d, V,
-                     dropout);
+  if (x_bf16)
+    hipLaunchKernelGGL(embedding_fwd_kernel<true>, dim3((M + 3) / 4), dim3(256), 0, stream, ids, wte, wpe, x, M, T, d,
+                       V, dropout);
+  else
+    hipLaunchKernelGGL(embedding_fwd_kernel<false>, dim3((M + 3) / 4), dim3(256), 0, stream, ids, wte, wpe, x, M, T,
+                       d, V, dropout);
   return hipGetLastError();
 }
 

@@ -24,12 +24,13 @@ struct DropoutArgs {
 };
 
 struct LnFwdArgs {
-  const float* x;      // [M, d] residual stream
+  const void* x;       // [M, d] residual stream (f32, or bf16 with x_bf16)
+  bool x_bf16;
   const void* delta;   // [M, d] optional update added to x (bf16 or f32)
   bool delta_bf16;
   const float* w;
   const float* b;
-  float* xs_out;       // [M, d] x + delta (only written when delta != nullptr)
+  void* xs_out;        // [M, d] x + delta, x's dtype (only written when delta != nullptr)
   void* y;             // [M, d] normalised output (bf16 or f32)
   bool y_bf16;
   float* mean;         // [M]
@@ -43,13 +44,15 @@ hipError_t launch_add_layernorm_fwd(const LnFwdArgs& a, hipStream_t stream);
 struct LnBwdArgs {
   const void* dy;      // [M, d] (bf16 or f32)
   bool dy_bf16;
-  const float* xs;
+  const void* xs;        // [M, d] saved residual (f32, or bf16 with xs_bf16)
+  bool xs_bf16;
   const float* mean;
   const float* rstd;
   const float* w;
-  const float* dresid;   // optional [M, d] gradient added to dx
+  const void* dresid;    // optional [M, d] gradient added to dx (the gradient stream's dtype)
+  bool grad_bf16;        // residual-gradient stream (dresid, dx) in bf16 instead of f32
   const float* dy_scale; // optional device scalar multiplying dy
-  float* dx;             // [M, d]
+  void* dx;              // [M, d]
   void* dx_lp;           // optional [M, d] copy of dx in dy's dtype
   float* dw;             // [d] accumulated
   float* db;             // [d] accumulated
@@ -89,7 +92,7 @@ hipError_t launch_colsum_accum(const void* dy, bool bf16, float* out, float* ws,
                                hipStream_t stream);
 // x[b*T+t] = wte[ids] + wpe[t]
 // x = dropout(wte[ids] + wpe[t]); the backward applies the same mask to dx before the scatter
-hipError_t launch_embedding_fwd(const int64_t* ids, const float* wte, const float* wpe, float* x,
+hipError_t launch_embedding_fwd(const int64_t* ids, const float* wte, const float* wpe, void* x, bool x_bf16,
                                 int B, int T, int d, int V, DropoutArgs dropout, hipStream_t stream);
 hipError_t launch_embedding_bwd(const float* dx, const int64_t* ids, float* dwte, float* dwpe,
                                 int B, int T, int d, int V, DropoutArgs dropout, hipStream_t stream);

@@ -11,6 +11,7 @@
 // register partials over a grid-stride run of rows, a cross-wave LDS reduction, then one fp32
 // atomic per column per workgroup.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include "kernels.h"
@@ -43,20 +44,28 @@ __device__ __forceinline__ void store4<bf16_raw>(bf16_raw* p, float4_t v) {
   *reinterpret_cast<ushort4_t*>(p) = o;
 }
 
+// the value a bf16 store would keep (round to nearest even), as fp32
+__device__ __forceinline__ float4_t round_bf16x4(float4_t v) {
+  return float4_t{bf2f(f2bf(v[0])), bf2f(f2bf(v[1])), bf2f(f2bf(v[2])), bf2f(f2bf(v[3]))};
+}
+
 constexpr int kLnWaves = 4;  // rows per workgroup in the forward
 
-// MAXC = max float4 chunks per lane = ceil(d / 4 / 64)
-template <int MAXC, typename TD, typename TY>
+// MAXC = max float4 chunks per lane = ceil(d / 4 / 64); TX = storage type of the residual stream
+// (x in, x + delta out): float, or bf16 for the engine's bf16 residual option, in which case the
+// sum is rounded to bf16 BEFORE the statistics, so the backward's x-hat of the stored value is the
+// forward's exactly (the add and the statistics themselves stay fp32 in registers)
+template <int MAXC, typename TD, typename TY, typename TX>
 __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
-    const float* __restrict__ x, const TD* __restrict__ delta, const float* __restrict__ w,
-    const float* __restrict__ b, float* __restrict__ xs_out, TY* __restrict__ y,
+    const TX* __restrict__ x, const TD* __restrict__ delta, const float* __restrict__ w,
+    const float* __restrict__ b, TX* __restrict__ xs_out, TY* __restrict__ y,
     float* __restrict__ mean_out, float* __restrict__ rstd_out, int M, int d, float eps, DropoutArgs dr) {
   resolve_dropout(dr);
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * kLnWaves + (threadIdx.x >> 6);
   if (row >= M) return;
   const int nc = d >> 2;
-  const float* xr = x + row * d;
+  const TX* xr = x + row * d;
   // unconditional loads (lanes past the row end read column 0 and are zeroed): a load under a
   // divergent `if` gets a vmcnt(0) at the branch join, one HBM round trip per 256-column chunk
   // gamma / beta are loaded with the row (on gfx950 vmcnt also counts stores: loading them after
@@ -87,6 +96,7 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
         for (int t = 0; t < 4; ++t) dv[j][t] = drop_keep(dr.seed, dr.thr, e0 + t) ? dv[j][t] * dr.scale : 0.f;
       }
       v[j] += dv[j];
+      if (!std::is_same<TX, float>::value) v[j] = round_bf16x4(v[j]);
       if (c < nc) store4(xs_out + row * d + 4 * c, v[j]);
     }
     if (c >= nc) v[j] = float4_t{0.f, 0.f, 0.f, 0.f};
@@ -118,9 +128,11 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
 
 constexpr int kBwdWaves = 4;
 
-// plain loads / stores of the fp32 operands (non-temporal hints measured as noise, git history)
-__device__ __forceinline__ float4_t load4_nt(const float* p) { return *reinterpret_cast<const float4_t*>(p); }
-__device__ __forceinline__ void store4_nt(float* p, float4_t v) { *reinterpret_cast<float4_t*>(p) = v; }
+// plain loads / stores of the residual operands (non-temporal hints measured as noise, git history)
+template <typename T>
+__device__ __forceinline__ float4_t load4_nt(const T* p) { return load4(p); }
+template <typename T>
+__device__ __forceinline__ void store4_nt(T* p, float4_t v) { store4(p, v); }
 
 // Lean backward (rows of <= 768 columns; the split-row kernel below takes wider rows), built for
 // latency hiding rather than for the fewest instructions:
@@ -134,11 +146,13 @@ __device__ __forceinline__ void store4_nt(float* p, float4_t v) { *reinterpret_c
 // The side stream's weight-gradient GEMM (wgrad_kernel<4,4>: 74 VGPRs + 256 AGPRs = 336 of a
 // SIMD's 512) leaves 176 registers per SIMD, so what LayerNorm backward has in flight on the CUs
 // that GEMM holds is bounded by load-destination registers, not by wave count.
-template <int MAXC, int ROWS, typename TDY, bool LOWP_OUT>
+// TX: storage type of the saved residual xs; TG: of the residual-gradient stream (dresid in, dx out):
+// float, or bf16 for the engine's bf16 residual / gradient-stream options (row math stays fp32)
+template <int MAXC, int ROWS, typename TDY, bool LOWP_OUT, typename TX, typename TG>
 __global__ __launch_bounds__(256, ROWS == 1 ? (MAXC <= 3 ? 4 : 2) : 3) void ln_bwd_lean_kernel(
-    const TDY* __restrict__ dy, const float* __restrict__ xs, const float* __restrict__ mean,
-    const float* __restrict__ rstd, const float* __restrict__ w, const float* __restrict__ dresid,
-    const float* __restrict__ dy_scale, float* __restrict__ dx, TDY* __restrict__ dx_lp,
+    const TDY* __restrict__ dy, const TX* __restrict__ xs, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const float* __restrict__ w, const TG* __restrict__ dresid,
+    const float* __restrict__ dy_scale, TG* __restrict__ dx, TDY* __restrict__ dx_lp,
     float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dproj, int M, int d, DropoutArgs dr) {
   resolve_dropout(dr);
   extern __shared__ __attribute__((aligned(16))) float smem[];  // [kBwdWaves][d]
@@ -259,11 +273,11 @@ __global__ __launch_bounds__(256, ROWS == 1 ? (MAXC <= 3 ? 4 : 2) : 3) void ln_b
 // whole-row kernel's 256 did not.  The two halves' row sums meet in LDS (one barrier per row
 // pair, parity double-buffered); column partials and the per-wave dproj rows are summed over the
 // two row slots at the end (fixed order).
-template <int MAXC, typename TDY, bool LOWP_OUT>
+template <int MAXC, typename TDY, bool LOWP_OUT, typename TX, typename TG>
 __global__ __launch_bounds__(256, 3) void ln_bwd_split_kernel(
-    const TDY* __restrict__ dy, const float* __restrict__ xs, const float* __restrict__ mean,
-    const float* __restrict__ rstd, const float* __restrict__ w, const float* __restrict__ dresid,
-    const float* __restrict__ dy_scale, float* __restrict__ dx, TDY* __restrict__ dx_lp,
+    const TDY* __restrict__ dy, const TX* __restrict__ xs, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const float* __restrict__ w, const TG* __restrict__ dresid,
+    const float* __restrict__ dy_scale, TG* __restrict__ dx, TDY* __restrict__ dx_lp,
     float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dproj, int M, int d, DropoutArgs dr) {
   resolve_dropout(dr);
   constexpr int HC = (MAXC + 1) / 2;  // float4 chunks per lane for half a row
@@ -372,12 +386,12 @@ __global__ __launch_bounds__(256, 3) void ln_bwd_split_kernel(
   }
 }
 
-template <int MAXC>
-void launch_fwd_c(const LnFwdArgs& a, hipStream_t st) {
+template <int MAXC, typename TX>
+void launch_fwd_x(const LnFwdArgs& a, hipStream_t st) {
   dim3 grid((a.M + kLnWaves - 1) / kLnWaves), block(256);
-#define LN_FWD(TD, TY)                                                                        \
-  hipLaunchKernelGGL((add_ln_fwd_kernel<MAXC, TD, TY>), grid, block, 0, st, a.x,              \
-                     (const TD*)a.delta, a.w, a.b, a.xs_out, (TY*)a.y, a.mean, a.rstd, a.M, a.d, \
+#define LN_FWD(TD, TY)                                                                              \
+  hipLaunchKernelGGL((add_ln_fwd_kernel<MAXC, TD, TY, TX>), grid, block, 0, st, (const TX*)a.x,     \
+                     (const TD*)a.delta, a.w, a.b, (TX*)a.xs_out, (TY*)a.y, a.mean, a.rstd, a.M, a.d, \
                      a.eps, a.dropout)
   if (a.delta_bf16) {
     if (a.y_bf16) LN_FWD(bf16_raw, bf16_raw); else LN_FWD(bf16_raw, float);
@@ -387,13 +401,38 @@ void launch_fwd_c(const LnFwdArgs& a, hipStream_t st) {
 #undef LN_FWD
 }
 
+template <int MAXC>
+void launch_fwd_c(const LnFwdArgs& a, hipStream_t st) {
+  if (a.x_bf16) launch_fwd_x<MAXC, bf16_raw>(a, st);
+  else launch_fwd_x<MAXC, float>(a, st);
+}
+
 // The backward kernel for this row width: the split-row kernel above 768 columns (GPT-2 XL
 // same-box +0.7 % over the whole-row lean kernel, profiles/r2/ab_ln_split_xl.txt), else the lean
 // kernel with one row per wave per iteration (two measured no better, git history)
+template <int MAXC, typename TDY, bool LP, typename TX, typename TG>
+const void* bwd_kernel_t() {
+  if (MAXC > 3) return (const void*)&ln_bwd_split_kernel<MAXC, TDY, LP, TX, TG>;
+  return (const void*)&ln_bwd_lean_kernel<MAXC, 1, TDY, LP, TX, TG>;
+}
+
+// residual storage combinations: 0 = fp32 xs / fp32 gradient stream, 1 = fp32 xs / bf16 gradient
+// stream, 2 = bf16 xs / bf16 gradient stream (an fp32-dy backward takes only 0)
+inline int res_mode(const LnBwdArgs& a) { return a.xs_bf16 ? 2 : (a.grad_bf16 ? 1 : 0); }
+
 template <int MAXC, typename TDY, bool LP>
-auto bwd_kernel() -> decltype(&ln_bwd_split_kernel<MAXC, TDY, LP>) {
-  if (MAXC > 3) return &ln_bwd_split_kernel<MAXC, TDY, LP>;
-  return &ln_bwd_lean_kernel<MAXC, 1, TDY, LP>;
+const void* bwd_kernel_r(int mode) {
+  if (mode == 2) return bwd_kernel_t<MAXC, TDY, LP, bf16_raw, bf16_raw>();
+  if (mode == 1) return bwd_kernel_t<MAXC, TDY, LP, float, bf16_raw>();
+  return bwd_kernel_t<MAXC, TDY, LP, float, float>();
+}
+
+template <int MAXC>
+const void* bwd_kernel(const LnBwdArgs& a) {
+  const int mode = res_mode(a);
+  if (a.dy_bf16) return a.dx_lp != nullptr ? bwd_kernel_r<MAXC, bf16_raw, true>(mode) : bwd_kernel_r<MAXC, bf16_raw, false>(mode);
+  return a.dx_lp != nullptr ? bwd_kernel_t<MAXC, float, true, float, float>()
+                            : bwd_kernel_t<MAXC, float, false, float, float>();
 }
 
 template <int MAXC>
@@ -401,18 +440,13 @@ int bwd_grid_c(const LnBwdArgs& a) {
   const size_t shm = (size_t)kBwdWaves * a.d * sizeof(float);
   // a whole number of resident waves of workgroups (a partial extra wave would be a pure tail:
   // every workgroup runs the same number of rows)
-  static int resident[2][2] = {{0, 0}, {0, 0}};
-  int& per_cu = resident[a.dy_bf16 ? 1 : 0][a.dx_lp != nullptr ? 1 : 0];
+  static int resident[3][2][2] = {};
+  int& per_cu = resident[res_mode(a)][a.dy_bf16 ? 1 : 0][a.dx_lp != nullptr ? 1 : 0];
   if (per_cu == 0) {
     int n = 0, dev = 0, cus = 0;
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (a.dy_bf16)
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, a.dx_lp ? bwd_kernel<MAXC, bf16_raw, true>()
-                                                              : bwd_kernel<MAXC, bf16_raw, false>(), 256, shm);
-    else
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, a.dx_lp ? bwd_kernel<MAXC, float, true>()
-                                                              : bwd_kernel<MAXC, float, false>(), 256, shm);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bwd_kernel<MAXC>(a), 256, shm);
     // one resident wave of workgroups (mb 32: 1 / 2 / 3 waves 950k / 944k / 936k tok/s, fewer
     // partial rows for the column sums; mb 128 flat: profiles/r2/ab_ln_waves_mb*.txt)
     per_cu = (n > 0 ? n : 4) * (cus > 0 ? cus : 256);
@@ -428,15 +462,12 @@ void launch_bwd_c(const LnBwdArgs& a, hipStream_t st) {
   float* pw = a.ws;
   float* pb = a.ws + (long)grid * a.d;
   float* pp = a.dproj != nullptr ? a.ws + 2L * grid * a.d : nullptr;
-  const void* fn = nullptr;
-  if (a.dy_bf16)
-    fn = (const void*)(a.dx_lp != nullptr ? bwd_kernel<MAXC, bf16_raw, true>() : bwd_kernel<MAXC, bf16_raw, false>());
-  else
-    fn = (const void*)(a.dx_lp != nullptr ? bwd_kernel<MAXC, float, true>() : bwd_kernel<MAXC, float, false>());
+  const void* fn = bwd_kernel<MAXC>(a);
   const void* dy = a.dy;
   void* dx_lp = a.dx_lp;
-  const float *xs = a.xs, *mean = a.mean, *rstd = a.rstd, *w = a.w, *dresid = a.dresid, *dy_scale = a.dy_scale;
-  float* dx = a.dx;
+  const void *xs = a.xs, *dresid = a.dresid;
+  const float *mean = a.mean, *rstd = a.rstd, *w = a.w, *dy_scale = a.dy_scale;
+  void* dx = a.dx;
   int M = a.M, d = a.d;
   DropoutArgs dr = a.dropout;
   void* args[] = {&dy, &xs, &mean, &rstd, &w, &dresid, &dy_scale, &dx, &dx_lp, &pw, &pb, &pp, &M, &d, &dr};

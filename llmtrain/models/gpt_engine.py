@@ -84,6 +84,9 @@ def accumulate_wgrad(dst: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> No
             if mode == "inplace":
                 raise
             _WGRAD_MODE[key] = "mm"
+    if dst.device.type != "cuda":  # CPU (tests): no fp32-output mm for bf16 operands
+        dst.add_(torch.mm(dy.t().float(), x.float()))
+        return
     dst.add_(torch.mm(dy.t(), x, out_dtype=torch.float32))
 
 
@@ -144,14 +147,30 @@ class _FusedLoss(torch.autograd.Function):
         return None, None, None, None, None
 
 
+RESIDUAL_MODES = ("fp32", "bf16_grad", "bf16")
+
+
 class FusedGPTEngine:
     """Owns the flat parameter store of a GPT and runs its fused forward/backward."""
 
     SIDE_LAG = 2  # blocks of side-stream GEMM operands kept alive before the main stream fences them
 
-    def __init__(self, model: Any, *, compute_dtype: torch.dtype = torch.bfloat16) -> None:
+    def __init__(self, model: Any, *, compute_dtype: torch.dtype = torch.bfloat16, residual: str = "fp32") -> None:
         self.model = model
         self.compute_dtype = compute_dtype
+        # storage of the residual stream (x, xs, xm: the LayerNorm inputs) and of its gradient
+        # (model.extra.residual_dtype): "fp32" (default; the reference's precision), "bf16_grad"
+        # (the backward's residual-gradient stream in bf16: LayerNorm backward moves 10 instead of
+        # 16 bytes per element) or "bf16" (both streams in bf16: 8 + 8 instead of 12 + 16).  The
+        # adds, LayerNorm statistics and row math stay fp32 in registers either way; the bf16 forms
+        # round the stored values (docs/round6.md §4 has the parity measurement that gates them)
+        if residual not in RESIDUAL_MODES:
+            raise ValueError(f"residual_dtype must be one of {RESIDUAL_MODES}, not {residual!r}")
+        if residual != "fp32" and compute_dtype != torch.bfloat16:
+            raise ValueError("a bf16 residual stream needs the bf16 compute dtype")
+        self.residual = residual
+        self.res_dtype = torch.bfloat16 if residual == "bf16" else torch.float32
+        self.grad_dtype = torch.float32 if residual == "fp32" else torch.bfloat16
         self.blocks = list(model.blocks)
         self.n_heads = model.n_heads
         self.head_dim = model.d_model // model.n_heads
@@ -327,7 +346,9 @@ class FusedGPTEngine:
             row_w = torch.full((n_tok,), 1.0 / n_tok, dtype=torch.float32, device=ids.device)
 
         self._push("fwd.embed")
-        x = ops.embedding_fwd(ids, m.token_embedding.weight, m.position_embedding.weight, dropout=state.site(0))
+        x = ops.embedding_fwd(
+            ids, m.token_embedding.weight, m.position_embedding.weight, dropout=state.site(0), out_dtype=self.res_dtype
+        )
         self._pop()
         delta: torch.Tensor | None = None
         for i, blk in enumerate(self.blocks):
@@ -418,7 +439,7 @@ class FusedGPTEngine:
         n_layers = len(self.blocks)
         dx, dx_lp = ops.layernorm_bwd(
             dhf, st.xf, st.muf, st.rsf, m.ln_f.weight, None, self._g(m.ln_f.weight), self._g(m.ln_f.bias),
-            go, want_lowp=True, dropout=st.site(3 * n_layers),
+            go, want_lowp=True, dropout=st.site(3 * n_layers), grad_dtype=self.grad_dtype,
         )
         del dhf
         self._notify("ln_f")
@@ -443,7 +464,7 @@ class FusedGPTEngine:
             # ln_2's dgamma / dbeta partial rows wait for ln_1's: one reduce launch per block
             dxm, dy_lp, ln2_parts = ops.layernorm_bwd(
                 dh2, a.xm, a.mu2, a.rs2, blk.ln_2.weight, dx, self._g(blk.ln_2.weight), self._g(blk.ln_2.bias),
-                None, want_lowp=True, dropout=st.site(1 + 3 * i), defer_params=True,
+                None, want_lowp=True, dropout=st.site(1 + 3 * i), defer_params=True, grad_dtype=self.grad_dtype,
             )
             del dh2, dx, dx_lp
             if st.keep_col is not None:  # gradient of y * keep: padded rows feed nothing back
@@ -472,6 +493,7 @@ class FusedGPTEngine:
             dx, dx_lp, ln1_parts = ops.layernorm_bwd(
                 dh1, a.xs, a.mu1, a.rs1, blk.ln_1.weight, dxm, self._g(blk.ln_1.weight), self._g(blk.ln_1.bias),
                 None, want_lowp=i > 0, dropout=st.site(3 * i) if i > 0 else (0.0, 0), defer_params=True,
+                grad_dtype=self.grad_dtype,
             )
             ops.ln_param_reduce(
                 [ln2_parts, ln1_parts],

@@ -144,7 +144,7 @@ def add_layernorm_fwd(x, delta, weight, bias, eps: float, out_dtype: torch.dtype
 
 def layernorm_bwd(
     dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale=None, *, want_lowp=False, dproj_bias=None,
-    dropout=(0.0, 0), defer_params=False,
+    dropout=(0.0, 0), defer_params=False, grad_dtype=torch.float32,
 ):
     """LayerNorm backward with two optional fusions for the producer of the normalised input:
 
@@ -152,32 +152,35 @@ def layernorm_bwd(
       whose output was added to the residual stream), and
     * ``dproj_bias`` (fp32 ``[d]``) accumulates ``colsum(dx)`` — that projection's bias grad;
 
-    both see the branch's dropout mask ``dropout = (p, site_seed)`` (the fp32 ``dx`` of the
-    residual stream itself does not).  Returns ``(dx_fp32, dx_lowp | None)``.
+    both see the branch's dropout mask ``dropout = (p, site_seed)`` (the residual-stream ``dx``
+    itself does not).  Returns ``(dx, dx_lowp | None)``.  ``grad_dtype``: storage of the
+    residual-gradient stream (``dresid`` in, ``dx`` out) — fp32, or bf16 for the engine's bf16
+    gradient stream, where ``dx_lowp`` without dropout IS ``dx`` (one write, not two).
 
     ``defer_params``: dgamma / dbeta are NOT accumulated yet; a third value ``parts`` (partial rows,
     ``[2, rows, d]``) goes to :func:`ln_param_reduce`, which reduces two LayerNorms in one launch.
     """
     p, seed = dropout
+    glp = grad_dtype == torch.bfloat16
     if defer_params:
         if dproj_bias is not None:
             raise ValueError("layernorm_bwd: defer_params takes no dproj_bias")
         if _on_gpu(dy):
             dx, dx_lp, parts = hip_ops().layernorm_bwd_deferred(
-                dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale, want_lowp, p, seed
+                dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale, want_lowp, p, seed, glp
             )
             return dx, (dx_lp if want_lowp else None), parts
         pw, pb = torch.zeros_like(dweight), torch.zeros_like(dbias)
-        dx = ref.layernorm_bwd(dy, xs, mean, rstd, weight, dresid, pw, pb, dy_scale)
-        branch = ref._apply_dropout(dx, p, seed)
+        dx = ref.layernorm_bwd(dy, xs, mean, rstd, weight, dresid, pw, pb, dy_scale, grad_dtype)
+        branch = ref._apply_dropout(dx.float(), p, seed)
         return dx, (branch.to(dy.dtype) if want_lowp else None), torch.stack([pw, pb])[:, None, :]
     if _on_gpu(dy):
         dx, dx_lp = hip_ops().layernorm_bwd(
-            dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale, want_lowp, dproj_bias, p, seed
+            dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale, want_lowp, dproj_bias, p, seed, glp
         )
         return dx, (dx_lp if want_lowp else None)
-    dx = ref.layernorm_bwd(dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale)
-    branch = ref._apply_dropout(dx, p, seed)
+    dx = ref.layernorm_bwd(dy, xs, mean, rstd, weight, dresid, dweight, dbias, dy_scale, grad_dtype)
+    branch = ref._apply_dropout(dx.float(), p, seed)
     if dproj_bias is not None:
         ref.colsum_accum(branch, dproj_bias)
     return dx, (branch.to(dy.dtype) if want_lowp else None)
@@ -234,17 +237,20 @@ def colsum_accum(dy, out) -> None:
         ref.colsum_accum(dy, out)
 
 
-def embedding_fwd(ids, wte, wpe, dropout=(0.0, 0)):
+def embedding_fwd(ids, wte, wpe, dropout=(0.0, 0), out_dtype=torch.float32):
+    """Token + position embedding (+ dropout), ``out_dtype`` = the residual stream's storage."""
     p, seed = dropout
     if _on_gpu(ids):
-        return hip_ops().embedding_fwd(ids, wte, wpe, p, seed)
-    return ref.embedding_fwd(ids, wte, wpe, p, seed)
+        return hip_ops().embedding_fwd(ids, wte, wpe, p, seed, out_dtype == torch.bfloat16)
+    return ref.embedding_fwd(ids, wte, wpe, p, seed, out_dtype)
 
 
 def embedding_bwd(dx, ids, dwte, dwpe, dropout=(0.0, 0)) -> None:
+    """Token / position embedding gradients from the residual-stream gradient ``dx`` (a bf16
+    gradient stream is widened once here: the scatter kernels read fp32 rows)."""
     p, seed = dropout
     if _on_gpu(dx):
-        hip_ops().embedding_bwd(dx, ids, dwte, dwpe, p, seed)
+        hip_ops().embedding_bwd(dx.float(), ids, dwte, dwpe, p, seed)
     else:
         ref.embedding_bwd(dx, ids, dwte, dwpe, p, seed)
 

@@ -117,15 +117,18 @@ def add_layernorm_fwd(
     dropout_p: float = 0.0,
     dropout_seed: int = 0,
 ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
-    """``xs = x + dropout(delta)`` (fp32 residual update), ``y = LN(xs)`` cast to ``out_dtype``.
+    """``xs = x + dropout(delta)`` (fp32 add), ``y = LN(xs)`` cast to ``out_dtype``.
 
-    Returns ``(xs, y, mean, rstd)``; when ``delta`` is None ``xs`` is ``x`` itself.
+    Returns ``(xs, y, mean, rstd)``; when ``delta`` is None ``xs`` is ``x`` itself.  A bf16 ``x``
+    (the engine's bf16 residual stream) gives a bf16 ``xs``, and the statistics are those of the
+    rounded ``xs`` (as the HIP kernel computes them).
     """
-    xs = x if delta is None else x + _apply_dropout(delta.float(), dropout_p, dropout_seed)
-    mean = xs.mean(dim=-1)
-    var = (xs - mean[:, None]).pow(2).mean(dim=-1)
+    xs = x if delta is None else (x.float() + _apply_dropout(delta.float(), dropout_p, dropout_seed)).to(x.dtype)
+    xs32 = xs.float()
+    mean = xs32.mean(dim=-1)
+    var = (xs32 - mean[:, None]).pow(2).mean(dim=-1)
     rstd = torch.rsqrt(var + eps)
-    y = (xs - mean[:, None]) * rstd[:, None] * weight.float() + bias.float()
+    y = (xs32 - mean[:, None]) * rstd[:, None] * weight.float() + bias.float()
     return xs, y.to(out_dtype), mean, rstd
 
 
@@ -139,8 +142,10 @@ def layernorm_bwd(
     dweight: torch.Tensor,
     dbias: torch.Tensor,
     dy_scale: torch.Tensor | None = None,
+    grad_dtype: torch.dtype = torch.float32,
 ) -> torch.Tensor:
-    """LayerNorm backward. Returns ``dx`` (fp32) = ``dresid + dLN/dx``; accumulates dγ, dβ.
+    """LayerNorm backward. Returns ``dx`` = ``dresid + dLN/dx`` (fp32 math, stored as
+    ``grad_dtype``: bf16 for the engine's bf16 gradient stream); accumulates dγ, dβ.
 
     ``dy_scale`` (0-d fp32 tensor) multiplies ``dy`` first (used to fold the loss gradient
     scale into the first backward kernel without a host sync).
@@ -148,14 +153,14 @@ def layernorm_bwd(
     g = dy.float()
     if dy_scale is not None:
         g = g * dy_scale.float()
-    xhat = (xs - mean[:, None]) * rstd[:, None]
+    xhat = (xs.float() - mean[:, None]) * rstd[:, None]
     dweight += (g * xhat).sum(dim=0)
     dbias += g.sum(dim=0)
     gw = g * weight.float()
     dx = rstd[:, None] * (gw - gw.mean(dim=-1, keepdim=True) - xhat * (gw * xhat).mean(dim=-1, keepdim=True))
     if dresid is not None:
-        dx = dx + dresid
-    return dx
+        dx = dx + dresid.float()
+    return dx.to(grad_dtype)
 
 
 def cross_entropy_fwd_bwd(
@@ -205,12 +210,13 @@ def colsum_accum(dy: torch.Tensor, out: torch.Tensor) -> None:
 
 
 def embedding_fwd(
-    ids: torch.Tensor, wte: torch.Tensor, wpe: torch.Tensor, dropout_p: float = 0.0, dropout_seed: int = 0
+    ids: torch.Tensor, wte: torch.Tensor, wpe: torch.Tensor, dropout_p: float = 0.0, dropout_seed: int = 0,
+    out_dtype: torch.dtype = torch.float32,
 ) -> torch.Tensor:
-    """``x[b*T+t] = dropout(wte[ids[b,t]] + wpe[t])`` → ``[B*T, d]`` fp32."""
+    """``x[b*T+t] = dropout(wte[ids[b,t]] + wpe[t])`` → ``[B*T, d]`` (fp32 math, ``out_dtype``)."""
     bsz, seqlen = ids.shape
     x = wte.float()[ids.reshape(-1)] + wpe.float()[:seqlen].repeat(bsz, 1)
-    return _apply_dropout(x, dropout_p, dropout_seed)
+    return _apply_dropout(x, dropout_p, dropout_seed).to(out_dtype)
 
 
 def embedding_bwd(

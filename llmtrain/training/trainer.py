@@ -194,7 +194,10 @@ class Trainer:
         self.tuned_gemms = enable_tuned_gemms(self._device)  # shipped hipBLASLt solution table (GPU)
         model = model.to(self._device)
         if self._policy.use_fused:
-            model.prepare_runtime(compute_dtype=self._policy.compute_dtype)
+            kw = {}
+            if "residual_dtype" in cfg.model.extra:  # fused engine option (gpt_engine.RESIDUAL_MODES)
+                kw["residual"] = str(cfg.model.extra["residual_dtype"])
+            model.prepare_runtime(compute_dtype=self._policy.compute_dtype, **kw)
         self._model: nn.Module = model
         if self._is_ddp_active:
             self._model = wrap_data_parallel(model, cfg, self._device)

@@ -37,7 +37,7 @@ def _oracle(qkv: torch.Tensor, B: int, T: int, H: int, key_valid: torch.Tensor |
     return out.detach(), x.grad.detach(), live
 
 
-def _check(name: str, got: torch.Tensor, want: torch.Tensor, rows_dim_last: int) -> None:
+def _check(name: str, got: torch.Tensor, want: torch.Tensor, rows_dim_last: int, slack: float = 6e-2) -> None:
     got, want = got.float(), want.float()
     # tensor-wide: relative Frobenius error (bf16 operands, fp32 accumulation)
     rel = (got - want).norm() / want.norm().clamp_min(1e-12)
@@ -46,7 +46,7 @@ def _check(name: str, got: torch.Tensor, want: torch.Tensor, rows_dim_last: int)
     g2, w2 = got.reshape(-1, rows_dim_last), want.reshape(-1, rows_dim_last)
     row_err = (g2 - w2).norm(dim=1)
     row_ref = w2.norm(dim=1)
-    bad = row_err > 3e-2 * row_ref + 6e-2 * row_ref.mean()  # rows that cancel to ~0 (dq of query 0)
+    bad = row_err > 3e-2 * row_ref + slack * row_ref.mean()  # rows that cancel to ~0 (dq of query 0)
     assert not bool(bad.any()), f"{name}: {int(bad.sum())} rows off, first {bad.nonzero()[:4].flatten().tolist()}"
 
 
@@ -182,7 +182,9 @@ def test_attention_dropout_head_dims(gpu_device, hd: int, B: int, T: int, H: int
     torch.testing.assert_close(lse_g.cpu(), lse_r, atol=2e-3, rtol=2e-3)
     _check("out (dropout)", out_g.cpu(), out_r.detach(), hd)
     a, r = dq_g.view(B * T, 3, H, hd), dq_r.view(B * T, 3, H, hd)
+    # dq of query 0 is exactly 0 in exact arithmetic (one key: dS = P (dP - delta) = 0); the kernel's
+    # delta comes from the bf16 O, whose rounding the 1 / keep-probability scale amplifies
     for i, name in enumerate(("dq", "dk", "dv")):
-        _check(f"{name} (dropout)", a[:, i], r[:, i], hd)
+        _check(f"{name} (dropout)", a[:, i], r[:, i], hd, slack=0.15)
     want = dq_r.sum(dim=0)
     assert (dbias.cpu() - want).abs().max().item() < 2e-2 * want.abs().max().item()

@@ -149,3 +149,29 @@ def test_state_dict_roundtrip_after_flattening() -> None:
     fresh.load_state_dict(sd)
     for p, q in zip(fresh.parameters(), ref.parameters()):
         torch.testing.assert_close(p, q)
+
+
+@pytest.mark.parametrize("residual", ["bf16_grad", "bf16"])
+def test_bf16_residual_streams_track_autograd(residual: str) -> None:
+    """model.extra.residual_dtype on the engine's reference ops (bf16 compute): the residual stream
+    and / or its gradient stored in bf16 stays within bf16 rounding of fp32 autograd, and the
+    option is refused with an fp32 compute dtype."""
+    torch.manual_seed(0)
+    args = dict(vocab_size=100, block_size=16, d_model=64, n_layers=2, n_heads=4, d_ff=128, dropout=0.0)
+    ref = GPT(**args)
+    fused = copy.deepcopy(ref)
+    engine = fused.prepare_runtime(compute_dtype=torch.bfloat16, residual=residual)
+    assert engine.grad_dtype == torch.bfloat16
+    assert engine.res_dtype == (torch.bfloat16 if residual == "bf16" else torch.float32)
+    ids = torch.randint(0, 100, (3, 16))
+    labels = torch.randint(0, 100, (3, 16))
+    F.cross_entropy(ref(ids).reshape(-1, 100), labels.reshape(-1)).backward()
+    fused.flat_store.zero_grad()
+    fused.fused_loss(ids, labels).backward()
+    for (name, p), (_, q) in zip(fused.named_parameters(), ref.named_parameters()):
+        rel = ((p.grad.float() - q.grad).norm() / (q.grad.norm() + 1e-12)).item()
+        assert rel < 3e-2, f"{name}: {rel:.3e}"
+    with pytest.raises(ValueError, match="bf16 compute"):
+        GPT(**args).prepare_runtime(compute_dtype=torch.float32, residual=residual)
+    with pytest.raises(ValueError, match="residual_dtype"):
+        GPT(**args).prepare_runtime(compute_dtype=torch.bfloat16, residual="fp16")

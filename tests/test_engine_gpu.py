@@ -24,10 +24,14 @@ def _model(dev, **kw):
     return GPT(**args).to(dev)
 
 
-def test_fused_matches_module_path(gpu_device):
+@pytest.mark.parametrize("residual", ["fp32", "bf16_grad", "bf16"])
+def test_fused_matches_module_path(gpu_device, residual):
+    """bf16 fused path vs fp32 module autograd, for each residual-stream storage option
+    (model.extra.residual_dtype): the bf16 forms round the stored residual / gradient values and
+    stay inside the same bound."""
     ref_model = _model(gpu_device)
     fused = copy.deepcopy(ref_model)
-    engine = fused.prepare_runtime(compute_dtype=torch.bfloat16)
+    engine = fused.prepare_runtime(compute_dtype=torch.bfloat16, residual=residual)
     ids = torch.randint(0, 1000, (4, 256), device=gpu_device)
     labels = torch.randint(0, 1000, (4, 256), device=gpu_device)
 

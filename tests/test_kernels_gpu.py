@@ -73,6 +73,52 @@ def test_layernorm_bwd(gpu_device, M, d, with_proj, lowp):
         assert torch.equal(dp, torch.full((d,), 0.25, device=gpu_device))
 
 
+@pytest.mark.parametrize("M,d", [(4096, 768), (4099, 768), (513, 1600), (100, 64)])
+@pytest.mark.parametrize("mode", ["bf16_grad", "bf16"])
+@pytest.mark.parametrize("drop", [0.0, 0.2])
+def test_layernorm_bf16_residual_streams(gpu_device, M, d, mode, drop):
+    """The engine's bf16 residual options (model.extra.residual_dtype): a bf16 residual stream in
+    the forward (x, xs bf16; statistics of the rounded sum) and a bf16 gradient stream in the
+    backward (dresid in, dx out), against the fp32 reference fed the same bf16 values; without
+    dropout the bf16 GEMM operand IS dx (one buffer)."""
+    g = torch.Generator(device="cpu").manual_seed(M + d)
+    res_dt = torch.bfloat16 if mode == "bf16" else torch.float32
+    x = torch.randn(M, d, generator=g).to(gpu_device, res_dt)
+    delta = torch.randn(M, d, generator=g).to(gpu_device, torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(d, generator=g)).to(gpu_device)
+    b = (0.1 * torch.randn(d, generator=g)).to(gpu_device)
+    seed = ref.dropout_site_seed(5, 3)
+    xs, y, mu, rs = hip().add_layernorm_fwd(x, delta, w, b, 1e-5, torch.bfloat16, drop, seed)
+    xs_r, y_r, mu_r, rs_r = ref.add_layernorm_fwd(x, delta, w, b, 1e-5, torch.float32, drop, seed)
+    assert xs.dtype == res_dt
+    _close(xs, xs_r, 1e-6, 1e-6 if mode != "bf16" else 0.0, "xs")  # the same rounding
+    _close(mu, mu_r, 1e-5, 1e-5, "mean")
+    _close(rs, rs_r, 1e-4, 1e-4, "rstd")
+    _close(y, y_r, 2e-2, 1e-2, "y")
+
+    dy = torch.randn(M, d, generator=g).to(gpu_device, torch.bfloat16)
+    dres = torch.randn(M, d, generator=g).to(gpu_device, torch.bfloat16)
+    scale = torch.tensor(0.5, device=gpu_device)
+    dw, db = torch.zeros(d, device=gpu_device), torch.zeros(d, device=gpu_device)
+    dw_r, db_r = dw.clone(), db.clone()
+    dx, dx_lp = hip().layernorm_bwd(dy, xs, mu, rs, w, dres, dw, db, scale, True, None, drop, seed, True)
+    dx_r = ref.layernorm_bwd(dy, xs, mu, rs, w, dres, dw_r, db_r, scale, torch.float32)
+    assert dx.dtype == torch.bfloat16
+    _close(dx, dx_r, 1e-2, 8e-3, "dx (bf16 stream)")
+    _close(dx_lp, ref._apply_dropout(dx.float(), drop, seed), 1e-2, 8e-3, "dx_lp")
+    if drop == 0.0:
+        assert dx_lp.data_ptr() == dx.data_ptr()  # the operand is the stream itself
+    _close(dw, dw_r, 1e-2, 1e-4, "dgamma")
+    _close(db, db_r, 1e-2, 1e-4, "dbeta")
+    # embedding forward straight into a bf16 residual stream
+    ids = torch.randint(0, 300, (2, 64), generator=g).to(gpu_device)
+    wte = torch.randn(300, d, generator=g).to(gpu_device)
+    wpe = torch.randn(64, d, generator=g).to(gpu_device)
+    e = hip().embedding_fwd(ids, wte, wpe, drop, seed, True)
+    assert e.dtype == torch.bfloat16
+    assert torch.equal(e, ref.embedding_fwd(ids, wte, wpe, drop, seed, torch.bfloat16))
+
+
 @pytest.mark.parametrize("M,V,Vp", [(256, 50257, 50304), (1000, 50257, 50304), (64, 16, 64), (33, 1000, 1024)])
 def test_cross_entropy_fwd_bwd(gpu_device, M, V, Vp):
     g = torch.Generator(device="cpu").manual_seed(V)

@@ -98,8 +98,9 @@ def make_config(args: argparse.Namespace, world: int):
     gpu = args.device == "cuda"
     if not gpu:
         model.setdefault("extra", {})["fused"] = args.path == "fused"
-    if args.path == "fused" and args.residual != "fp32":
-        model.setdefault("extra", {})["residual_dtype"] = args.residual
+    residual = getattr(args, "residual", None)
+    if args.path == "fused" and residual is not None:
+        model.setdefault("extra", {})["residual_dtype"] = residual
     payload = {
         "schema_version": 1,
         # deterministic=False: the fast path's split-K / embedding atomics (run.deterministic
@@ -149,8 +150,9 @@ def main() -> int:
     ap.add_argument("--deterministic", action="store_true", help="fixed-order reductions (run.deterministic)")
     ap.add_argument("--cuda-graph", action="store_true",
                     help="capture the optimizer step as a hipGraph and replay it (1 GPU, dropout 0)")
-    ap.add_argument("--residual", choices=["fp32", "bf16_grad", "bf16"], default="fp32",
-                    help="fused engine: storage of the residual stream / its gradient (model.extra.residual_dtype)")
+    ap.add_argument("--residual", choices=["fp32", "bf16_grad", "bf16"], default=None,
+                    help="fused engine: storage of the residual stream / its gradient (model.extra.residual_dtype; "
+                         "default: the engine's, bf16 with bf16 compute)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo on GPU: rehearse the N-rank path on a box with fewer GPUs (ranks share devices)")
     args = ap.parse_args()
@@ -257,7 +259,7 @@ def main() -> int:
                 "deterministic": args.deterministic,
                 "backend": dist.get_backend() if world > 1 else None,
                 "cuda_graph": bool(args.cuda_graph),
-                "residual_dtype": args.residual,
+                "residual_dtype": getattr(getattr(raw, "engine", None), "residual", None),
             },
             "tokens_per_sec_per_gpu": round(tps / world, 1),
             "per_rank_tokens_per_sec": [round(r[1] / r[0], 1) for r in rows],

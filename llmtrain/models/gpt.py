@@ -186,12 +186,12 @@ class GPT(nn.Module):
             and self.d_ff % 8 == 0
         )
 
-    def prepare_runtime(self, *, compute_dtype: torch.dtype = torch.bfloat16, residual: str = "fp32") -> Any:
+    def prepare_runtime(self, *, compute_dtype: torch.dtype = torch.bfloat16, residual: str | None = None) -> Any:
         """Move parameters into flat buffers and build the fused engine (idempotent).
 
         Call after ``model.to(device)`` and before building the optimizer.  ``residual``: storage
-        of the residual stream and its gradient (``model.extra.residual_dtype``, see
-        :class:`~llmtrain.models.gpt_engine.FusedGPTEngine`).
+        of the residual stream and its gradient (``model.extra.residual_dtype``; None = bf16 with
+        the bf16 compute dtype, fp32 otherwise — see :class:`~llmtrain.models.gpt_engine.FusedGPTEngine`).
         """
         if self._engine is None:
             from llmtrain.models.gpt_engine import FusedGPTEngine

@@ -155,15 +155,22 @@ class FusedGPTEngine:
 
     SIDE_LAG = 2  # blocks of side-stream GEMM operands kept alive before the main stream fences them
 
-    def __init__(self, model: Any, *, compute_dtype: torch.dtype = torch.bfloat16, residual: str = "fp32") -> None:
+    def __init__(
+        self, model: Any, *, compute_dtype: torch.dtype = torch.bfloat16, residual: str | None = None
+    ) -> None:
         self.model = model
         self.compute_dtype = compute_dtype
         # storage of the residual stream (x, xs, xm: the LayerNorm inputs) and of its gradient
-        # (model.extra.residual_dtype): "fp32" (default; the reference's precision), "bf16_grad"
-        # (the backward's residual-gradient stream in bf16: LayerNorm backward moves 10 instead of
-        # 16 bytes per element) or "bf16" (both streams in bf16: 8 + 8 instead of 12 + 16).  The
-        # adds, LayerNorm statistics and row math stay fp32 in registers either way; the bf16 forms
-        # round the stored values (docs/round6.md §4 has the parity measurement that gates them)
+        # (model.extra.residual_dtype): "fp32" (the reference's precision; the default with an fp32
+        # compute dtype), "bf16_grad" (the backward's residual-gradient stream in bf16: LayerNorm
+        # backward moves 10 instead of 16 bytes per element) or "bf16" (both streams in bf16:
+        # 8 + 8 instead of 12 + 16; the default with the bf16 compute dtype, as in Megatron-style
+        # bf16 training without fp32 residual connections).  The adds, LayerNorm statistics and row
+        # math stay fp32 in registers either way; the bf16 forms round the stored values.  Measured
+        # (docs/round6.md §4): GPT-2 124M +3.6 % tok/s, -4.7 GiB peak, 1,500-step validation loss
+        # within the fp32-residual path's seed spread
+        if residual is None:
+            residual = "bf16" if compute_dtype == torch.bfloat16 else "fp32"
         if residual not in RESIDUAL_MODES:
             raise ValueError(f"residual_dtype must be one of {RESIDUAL_MODES}, not {residual!r}")
         if residual != "fp32" and compute_dtype != torch.bfloat16:

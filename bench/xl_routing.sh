@@ -16,6 +16,11 @@ env LLMTRAIN_FGEMM_MAX_A_MB=0 LLMTRAIN_FGEMM_ANY=none MB=16 BENCH_ARGS="--model 
   || { echo "tune failed"; tail -20 "$OUT/tune.log"; exit 1; }
 tail -12 gpurun_out/tunableop/tuned0.csv
 cp gpurun_out/tunableop/tuned0.csv "$OUT/tuned_xl.csv"
-cp gpurun_out/tunableop/tuned0.csv llmtrain/runtime/tuned/gemm_tunableop_gfx950.csv  # (the box's scratch copy)
+# the A/B below loads the box-tuned table in place of the shipped one; the shipped file is restored
+# on exit, so a run in a working tree cannot leave the box's table behind to be committed
+SHIPPED=llmtrain/runtime/tuned/gemm_tunableop_gfx950.csv
+cp "$SHIPPED" "$OUT/shipped_table_backup.csv"
+trap 'cp "$OUT/shipped_table_backup.csv" "$SHIPPED"' EXIT
+cp gpurun_out/tunableop/tuned0.csv "$SHIPPED"
 bash scripts/abn.sh "LLMTRAIN_FGEMM_MAX_A_MB=64" "LLMTRAIN_FGEMM_MAX_A_MB=0" "LLMTRAIN_FGEMM_NEVER=fwd" -- \
   --model gpt2-xl --micro-batch 16 --grad-accum 4 --deterministic --steps 4 --warmup 2 | tee "$OUT/ab_xl_det.txt"

@@ -42,6 +42,7 @@ Reference call sites replaced: ``models/gpt.py:49-74`` (attention), ``:86-105`` 
 from __future__ import annotations
 
 import os
+import warnings
 from collections.abc import Callable
 from dataclasses import dataclass, field
 from typing import Any
@@ -227,6 +228,9 @@ class FusedGPTEngine:
         # (LLMTRAIN_FUSED_GEMM=0: hipBLASLt everywhere + separate GELU passes)
         self.fused_gemm = os.environ.get("LLMTRAIN_FUSED_GEMM", "1") != "0"
         self.markers = os.environ.get("LLMTRAIN_ROCTX", "0") == "1" and self.store.device.type == "cuda"
+        # set by a Trainer with run.deterministic: warn once if a step runs outside its kernel policy
+        self.expect_deterministic = False
+        self._warned_policy = False
         self._side: torch.cuda.Stream | None = None
         self._pending: list[torch.Tensor] = []  # operands of side-stream GEMMs of the current block
         self._held: list[tuple[Any, list[torch.Tensor]]] = []  # (side event, operands) per block
@@ -308,6 +312,16 @@ class FusedGPTEngine:
     def loss(self, ids: torch.Tensor, labels: torch.Tensor, mask: torch.Tensor | None) -> torch.Tensor:
         if not self.fused_gemm and self.store.device.type == "cuda":
             ops._det_fallback("every GEMM (LLMTRAIN_FUSED_GEMM=0)")
+        if self.expect_deterministic and not self._warned_policy and self.store.device.type == "cuda" \
+                and not ops.policy_state()[0]["deterministic"]:
+            # a Trainer configured run.deterministic scopes its own steps (Trainer.kernel_policy);
+            # driving its model directly runs the fast path's atomics unless the caller scopes it
+            self._warned_policy = True
+            warnings.warn(
+                "run.deterministic is set for this model's Trainer but the process-wide kernel policy is "
+                "the fast (atomic) one here: wrap direct engine use in trainer.kernel_policy() or "
+                "llmtrain.ops.kernel_policy(True)", RuntimeWarning, stacklevel=3,
+            )
         self.store.sync_shadow()
         if torch.is_grad_enabled():
             return _FusedLoss.apply(self._anchor, self, ids, labels, mask)

@@ -197,7 +197,8 @@ class Trainer:
             kw = {}
             if "residual_dtype" in cfg.model.extra:  # fused engine option (gpt_engine.RESIDUAL_MODES)
                 kw["residual"] = str(cfg.model.extra["residual_dtype"])
-            model.prepare_runtime(compute_dtype=self._policy.compute_dtype, **kw)
+            engine = model.prepare_runtime(compute_dtype=self._policy.compute_dtype, **kw)
+            engine.expect_deterministic = bool(cfg.run.deterministic)
         self._model: nn.Module = model
         if self._is_ddp_active:
             self._model = wrap_data_parallel(model, cfg, self._device)

@@ -70,6 +70,11 @@ CASES = [
     # grids above take the per-key-block split with bf16 partial planes + reduce)
     (32, 300, 8, 48, "mixed"),
     (20, 1024, 12, 64, "mixed"),
+    # B*H = 512 = two per CU on 256 CUs: the 4-wave / two-workgroups-per-CU backward where built
+    # (csrc/attention_bwd.hip kBwdFourWaves), else the per-(b, h) 8-wave form
+    (64, 256, 8, 64, None),
+    (32, 300, 16, 64, "mixed"),
+    (64, 160, 8, 32, "mixed"),
 ]
 
 

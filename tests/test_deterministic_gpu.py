@@ -182,3 +182,26 @@ def test_deterministic_training_runs_are_bitwise_equal(schedule: str, monkeypatc
         torch.cuda.empty_cache()
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_direct_engine_use_outside_the_policy_warns_once() -> None:
+    """A Trainer configured run.deterministic scopes its own steps; driving its model directly
+    (outside trainer.kernel_policy()) runs the fast path's atomics, and the engine says so once."""
+    import warnings
+
+    from llmtrain.training.trainer import Trainer
+
+    cfg = _det_cfg()
+    cfg = type(cfg).model_validate({**cfg.model_dump(), "model": {**cfg.model_dump()["model"], "n_layers": 1}})
+    trainer = Trainer(cfg)
+    model = trainer.model
+    assert model.engine.expect_deterministic
+    ids = torch.randint(0, 50257, (2, 1024), device="cuda")
+    with warnings.catch_warnings(record=True) as seen:
+        warnings.simplefilter("always")
+        with trainer.kernel_policy():
+            model.fused_loss(ids, ids).backward()
+        assert not [w for w in seen if "kernel policy" in str(w.message)]
+        for _ in range(2):
+            model.fused_loss(ids, ids).backward()
+    assert len([w for w in seen if "kernel policy" in str(w.message)]) == 1

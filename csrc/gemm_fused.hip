@@ -65,6 +65,9 @@ constexpr int kSmemElems = NSLOT * kSlotElems + kWaves * kEpiFloats * 2;  // 160
 constexpr int kOob = 0x7ffffff0;                // buffer offset past any descriptor: dropped / 0
 constexpr int kBand = 4;                        // n-tiles per raster band (see tile_origin)
 constexpr int kWideM = 256;                     // from this many m-tiles on, one band spans all of N
+#ifndef LLMT_FGEMM_EPI_PROBE
+#define LLMT_FGEMM_EPI_PROBE 0  // 1: variant build without epilogues (timing probe, wrong results)
+#endif
 
 constexpr float kInvSqrt2 = 0.70710678118654752f;
 constexpr float kInvSqrt2Pi = 0.39894228040143268f;
@@ -392,7 +395,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
       mfma_group(acc, 0, a0, b1);
       if (g + 1 < total) {
         // stage g+1 was issued last, in iteration g-1; an epilogue after it iff g starts a tile
-        wait_ring<EpiOps<EPI>::value>(t > 0 && s == 0);
+        wait_ring<EpiOps<EPI>::value>(!LLMT_FGEMM_EPI_PROBE && t > 0 && s == 0);
         if (g + 2 < total) issue(g + 2);
         read_a(g + 1, 0, 0, a0);
         read_b(g + 1, 0, b0);
@@ -400,6 +403,20 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
       mfma_group(acc, 1, a1, b1);
     }
 
+#if LLMT_FGEMM_EPI_PROBE
+    // timing probe (variant builds only, wrong results): no epilogue — every accumulator feeds one
+    // sum whose store never happens, so the MFMAs stay; measures the main loop alone
+    // (profiles/r6/fgemm/probe_*.jsonl, docs/round6.md section 6)
+    {
+      float sink = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sink += acc[j][i][0] + acc[j][i][1] + acc[j][i][2] + acc[j][i][3];
+      if (sink == 1.2345e38f) p.C[lane] = 0;
+      continue;
+    }
+#endif
     // ---------------- epilogue of tile t ----------------
     // per 16-row m-fragment: its four 16x16 accumulator tiles -> [16 m][64 n] fp32 LDS image
     // (16-byte chunks XOR (row & 15)) -> 8 lanes per row read 8 columns each -> one 16-byte store

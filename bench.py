@@ -101,6 +101,9 @@ def make_config(args: argparse.Namespace, world: int):
     residual = getattr(args, "residual", None)
     if args.path == "fused" and residual is not None:
         model.setdefault("extra", {})["residual_dtype"] = residual
+    mlp_store = getattr(args, "mlp_store", None)
+    if args.path == "fused" and mlp_store is not None:
+        model.setdefault("extra", {})["mlp_store"] = mlp_store
     payload = {
         "schema_version": 1,
         # deterministic=False: the fast path's split-K / embedding atomics (run.deterministic
@@ -153,6 +156,8 @@ def main() -> int:
     ap.add_argument("--residual", choices=["fp32", "bf16_grad", "bf16"], default=None,
                     help="fused engine: storage of the residual stream / its gradient (model.extra.residual_dtype; "
                          "default: the engine's, bf16 with bf16 compute)")
+    ap.add_argument("--mlp-store", choices=["u", "gd"], default=None,
+                    help="fused engine: what the MLP keeps for its backward (model.extra.mlp_store)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo on GPU: rehearse the N-rank path on a box with fewer GPUs (ranks share devices)")
     args = ap.parse_args()
@@ -260,6 +265,7 @@ def main() -> int:
                 "backend": dist.get_backend() if world > 1 else None,
                 "cuda_graph": bool(args.cuda_graph),
                 "residual_dtype": getattr(getattr(raw, "engine", None), "residual", None),
+                "mlp_store": getattr(getattr(raw, "engine", None), "mlp_store", None),
             },
             "tokens_per_sec_per_gpu": round(tps / world, 1),
             "per_rank_tokens_per_sec": [round(r[1] / r[0], 1) for r in rows],

@@ -51,8 +51,11 @@ def run_path(path: str, args: argparse.Namespace) -> dict:
     model = dict(MODELS[args.model], name="gpt", dropout=args.dropout, tie_embeddings=True)
     fused = path.split(":")[0] == "fused"
     model["extra"] = {"fused": fused}
-    if fused and ":" in path:
-        model["extra"]["residual_dtype"] = path.split(":", 1)[1]
+    if fused and ":" in path:  # fused:<residual_dtype>[:<mlp_store>]
+        opts = path.split(":")[1:]
+        model["extra"]["residual_dtype"] = opts[0]
+        if len(opts) > 1:
+            model["extra"]["mlp_store"] = opts[1]
     precision = "fp32" if path == "module_fp32" else "bf16"
     if args.device == "cpu":
         precision = "fp32"

@@ -538,7 +538,9 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tens
   const int64_t N = b_kn ? b.size(1) : b.size(0);
   TORCH_CHECK((b_kn ? b.size(0) : b.size(1)) == K, "gemm_fused: inner dimensions differ");
   TORCH_CHECK(K % 64 == 0 && K >= 256 && N % 8 == 0, "gemm_fused: needs K % 64 == 0, K >= 256, N % 8 == 0");
-  TORCH_CHECK(epilogue >= 0 && epilogue <= 3, "gemm_fused: epilogue must be 0, 1, 2 or 3");
+  TORCH_CHECK(epilogue >= 0 && epilogue <= 5, "gemm_fused: epilogue must be 0-5");
+  const bool has_u = epilogue == 2 || epilogue == 3 || epilogue == 5;
+  const bool gelu_out = epilogue == 1 || epilogue == 4;
   // the kernel's buffer descriptors and tile offsets are 32-bit byte offsets: every operand and
   // output (a [M,K], b, out / u / c2 [M,N]) must stay below 2 GiB, else loads read zeros and
   // stores drop silently — callers split larger GEMMs into row chunks (llmtrain/ops, _gemm_rows)
@@ -574,14 +576,14 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tens
   c10::optional<Tensor> out2;
   g.c = out.data_ptr();
   g.ldc = (int)N;
-  if (bias.has_value() && epilogue != 2) {
+  if (bias.has_value() && !has_u) {
     check_gpu(*bias, "bias");
     check_dtype(*bias, at::kBFloat16, "bias");
     TORCH_CHECK(bias->numel() == N, "gemm_fused: bias must have N elements");
     TORCH_CHECK((uintptr_t)bias->data_ptr() % 4 == 0, "gemm_fused: bias must be 4-byte aligned");
     g.bias = bias->data_ptr();
   }
-  if (epilogue == 1) {
+  if (gelu_out) {
     out2 = at::empty({M, N}, a.options());
     g.c2 = out2->data_ptr();
   }
@@ -591,7 +593,7 @@ std::tuple<Tensor, c10::optional<Tensor>> gemm_fused(const Tensor& a, const Tens
     g.delta = out2->data_ptr<float>();
     g.T = (int)seq_len;
   }
-  if (epilogue >= 2) {
+  if (has_u) {
     TORCH_CHECK(u.has_value(), "gemm_fused: epilogue 2/3 needs u");
     check_gpu(*u, "u");
     check_dtype(*u, at::kBFloat16, "u");

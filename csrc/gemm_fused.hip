@@ -8,6 +8,9 @@
 //   1  U = bf16(acc + bias), C2 = bf16(gelu(U))  (fc forward: pre-activation kept for backward)
 //   2  C = bf16(acc * gelu'(U)), dbias += colsum(C)   (proj dX: GELU backward + fc bias grad)
 //   3  C = bf16(acc), delta[b, h, t] = sum_d C[m, 64h + d] * U[m, 64h + d], dbias += colsum(C)
+//   4  u = bf16(acc + bias), C = bf16(gelu'(u)), C2 = bf16(gelu(u))  (fc forward keeping the GELU
+//      derivative instead of the pre-activation: the backward's epilogue 5 then skips the erf math)
+//   5  C = bf16(acc * U), dbias += colsum(C)  (U = the stored gelu'(u): proj dX + GELU backward)
 //      (attention out-proj dX = dO; U = the attention output O: the flash-attention backward's
 //      row constant and, without dropout, the V part of the qkv bias gradient — each wave's 64
 //      output columns are exactly one head, so the per-head dot product never leaves the wave)
@@ -96,7 +99,7 @@ __device__ __forceinline__ float gelu_grad(float u) {
 // VMEM ops each epilogue issues unconditionally (a lower bound is what the counted waits need)
 template <int EPI>
 struct EpiOps {
-  static constexpr int value = EPI == 0 ? 16 : (EPI == 3 ? 48 : 32);
+  static constexpr int value = EPI == 0 ? 16 : (EPI == 3 ? 48 : 32);  // 4 as 1, 5 as 2
 };
 
 // one 256-byte LDS-DMA op (4 bytes per lane), M0 saved/restored like dma16
@@ -271,7 +274,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
 
   float* epi = reinterpret_cast<float*>(smem + NSLOT * kSlotElems) + wave * kEpiFloats;
   const unsigned epi_lds = (unsigned)(unsigned long)(lds_void*)epi;
-  const bool kBiasDma = EPI != 2 && p.bias != nullptr;
+  constexpr bool kHasU = EPI == 2 || EPI == 3 || EPI == 5;  // an [M, N] bf16 operand read per row segment
+  constexpr bool kGelu = EPI == 1 || EPI == 4;              // second output C2 = gelu(u)
+  const bool kBiasDma = !kHasU && p.bias != nullptr;
   const __amdgpu_buffer_rsrc_t rbias = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(kBiasDma ? p.bias : p.A), (short)0, kBiasDma ? p.N * 2 : 0, 0x00020000);
 
@@ -324,9 +329,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
   const __amdgpu_buffer_rsrc_t rc =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.C, (short)0, p.M * p.ldc * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t rc2 = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(EPI == 1 ? p.C2 : p.C), (short)0, p.M * p.ldc * 2, 0x00020000);
+      (void*)(kGelu ? p.C2 : p.C), (short)0, p.M * p.ldc * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(EPI >= 2 ? p.U : p.C), (short)0, p.M * (EPI >= 2 ? p.ldu : p.ldc) * 2, 0x00020000);
+      (void*)(kHasU ? p.U : p.C), (short)0, p.M * (kHasU ? p.ldu : p.ldc) * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t rdel = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(EPI == 3 ? p.delta : (float*)p.C), (short)0, EPI == 3 ? p.M * (p.N / 64) * 4 : 0, 0x00020000);
 
@@ -451,11 +456,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
                         : __builtin_amdgcn_raw_buffer_load_b128(ru, uoff, 0, 0);
       }
     };
-    if (EPI >= 2) load_u(0, uraw[0]);
+    if (kHasU) load_u(0, uraw[0]);
 #pragma unroll
     for (int mf = 0; mf < 8; ++mf) {
       __builtin_amdgcn_sched_barrier(0);
-      if (EPI >= 2 && mf + 1 < 8) load_u(mf + 1, uraw[(mf + 1) & 1]);
+      if (kHasU && mf + 1 < 8) load_u(mf + 1, uraw[(mf + 1) & 1]);
       {
         const int row = lane & 15;
 #pragma unroll
@@ -509,7 +514,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
           asm volatile("" : "+v"(csum[0]), "+v"(csum[1]), "+v"(csum[2]), "+v"(csum[3]), "+v"(csum[4]),
                        "+v"(csum[5]), "+v"(csum[6]), "+v"(csum[7]));
         }
-      } else if (EPI == 2) {
+      } else if (EPI == 2 || EPI == 5) {
 #pragma unroll
         for (int it = 0; it < 2; ++it) {
           __builtin_amdgcn_sched_barrier(0);  // one row segment at a time: bounded VGPR pressure
@@ -517,7 +522,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
           float o[8];
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            o[k] = bf2f(f2bf(vals[it][k] * gelu_grad(bf2f(uv[k]))));
+            o[k] = EPI == 5 ? bf2f(f2bf(vals[it][k] * bf2f(uv[k]))) : bf2f(f2bf(vals[it][k] * gelu_grad(bf2f(uv[k]))));
             csum[k] += o[k];
           }
           st16(__builtin_bit_cast(u32x4, pack8(o)), rc, off[it]);
@@ -533,16 +538,29 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fused_kernel(Args p) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) o[k] = vals[it][k] + bias_f[k];
           const ushort8_t ov = pack8(o);
-          st16(__builtin_bit_cast(u32x4, ov), rc, off[it]);
-          if (EPI == 1) {
+          if (EPI == 4) {  // gelu'(u) and gelu(u) of the bf16 pre-activation, one erf evaluation
+            float gd[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) o[k] = gelu(bf2f(ov[k]));
+            for (int k = 0; k < 8; ++k) {
+              const float uu = bf2f(ov[k]);
+              const ErfPdf ep = erf_pdf(uu);
+              gd[k] = fmaf(0.5f, 1.f + ep.erf, uu * kInvSqrt2Pi * ep.e);
+              o[k] = 0.5f * uu * (1.f + ep.erf);
+            }
+            st16(__builtin_bit_cast(u32x4, pack8(gd)), rc, off[it]);
             st16(__builtin_bit_cast(u32x4, pack8(o)), rc2, off[it]);
+          } else {
+            st16(__builtin_bit_cast(u32x4, ov), rc, off[it]);
+            if (EPI == 1) {
+#pragma unroll
+              for (int k = 0; k < 8; ++k) o[k] = gelu(bf2f(ov[k]));
+              st16(__builtin_bit_cast(u32x4, pack8(o)), rc2, off[it]);
+            }
           }
         }
       }
     }
-    if (EPI >= 2 && p.dbias != nullptr) {  // column sums over the wave's 128 rows: lanes sharing q
+    if (kHasU && p.dbias != nullptr) {  // column sums over the wave's 128 rows: lanes sharing q
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float v = csum[k];
@@ -575,9 +593,10 @@ hipError_t launch_gemm_fused(const GemmFusedArgs& g, hipStream_t stream) {
   using namespace fgemm;
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
   if (g.K < 4 * BK || g.K % BK || g.N % 8 || g.lda % 8 || g.ldb % 8 || g.ldc % 8) return hipErrorInvalidValue;
-  if (g.epilogue < 0 || g.epilogue > 3) return hipErrorInvalidValue;
-  if (g.epilogue == 1 && g.c2 == nullptr) return hipErrorInvalidValue;
-  if (g.epilogue >= 2 && (g.u == nullptr || g.ldu % 8)) return hipErrorInvalidValue;
+  if (g.epilogue < 0 || g.epilogue > 5) return hipErrorInvalidValue;
+  const bool has_u = g.epilogue == 2 || g.epilogue == 3 || g.epilogue == 5;
+  if ((g.epilogue == 1 || g.epilogue == 4) && g.c2 == nullptr) return hipErrorInvalidValue;
+  if (has_u && (g.u == nullptr || g.ldu % 8)) return hipErrorInvalidValue;
   if (g.epilogue == 3 && (g.delta == nullptr || g.T <= 0 || g.M % g.T || g.N % 64 ||
                           (long long)g.M * (g.N / 64) * 4 >= (1LL << 31) - 64))
     return hipErrorInvalidValue;
@@ -621,7 +640,11 @@ hipError_t launch_gemm_fused(const GemmFusedArgs& g, hipStream_t stream) {
     case 4: launch_one<false, 2>(a, stream); break;
     case 5: launch_one<true, 2>(a, stream); break;
     case 6: launch_one<false, 3>(a, stream); break;
-    default: launch_one<true, 3>(a, stream); break;
+    case 7: launch_one<true, 3>(a, stream); break;
+    case 8: launch_one<false, 4>(a, stream); break;
+    case 9: launch_one<true, 4>(a, stream); break;
+    case 10: launch_one<false, 5>(a, stream); break;
+    default: launch_one<true, 5>(a, stream); break;
   }
   if (g.dbias != nullptr) return launch_colsum_reduce(g.ws, nparts, g.N, g.dbias, g.ws + (long)nparts * g.N, stream);
   return hipGetLastError();

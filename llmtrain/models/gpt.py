@@ -186,7 +186,9 @@ class GPT(nn.Module):
             and self.d_ff % 8 == 0
         )
 
-    def prepare_runtime(self, *, compute_dtype: torch.dtype = torch.bfloat16, residual: str | None = None) -> Any:
+    def prepare_runtime(
+        self, *, compute_dtype: torch.dtype = torch.bfloat16, residual: str | None = None, mlp_store: str | None = None
+    ) -> Any:
         """Move parameters into flat buffers and build the fused engine (idempotent).
 
         Call after ``model.to(device)`` and before building the optimizer.  ``residual``: storage
@@ -196,7 +198,7 @@ class GPT(nn.Module):
         if self._engine is None:
             from llmtrain.models.gpt_engine import FusedGPTEngine
 
-            self._engine = FusedGPTEngine(self, compute_dtype=compute_dtype, residual=residual)
+            self._engine = FusedGPTEngine(self, compute_dtype=compute_dtype, residual=residual, mlp_store=mlp_store)
         return self._engine
 
     @property

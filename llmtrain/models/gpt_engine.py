@@ -149,6 +149,7 @@ class _FusedLoss(torch.autograd.Function):
 
 
 RESIDUAL_MODES = ("fp32", "bf16_grad", "bf16")
+MLP_STORE_DEFAULT = "u"
 
 
 class FusedGPTEngine:
@@ -157,7 +158,8 @@ class FusedGPTEngine:
     SIDE_LAG = 2  # blocks of side-stream GEMM operands kept alive before the main stream fences them
 
     def __init__(
-        self, model: Any, *, compute_dtype: torch.dtype = torch.bfloat16, residual: str | None = None
+        self, model: Any, *, compute_dtype: torch.dtype = torch.bfloat16, residual: str | None = None,
+        mlp_store: str | None = None,
     ) -> None:
         self.model = model
         self.compute_dtype = compute_dtype
@@ -177,6 +179,14 @@ class FusedGPTEngine:
         if residual != "fp32" and compute_dtype != torch.bfloat16:
             raise ValueError("a bf16 residual stream needs the bf16 compute dtype")
         self.residual = residual
+        # what the MLP keeps for its backward (model.extra.mlp_store): "u", the fc pre-activation
+        # (the dX epilogue evaluates gelu'(u)), or "gd", gelu'(u) itself, formed by the fc GEMM's
+        # epilogue from the same erf as gelu(u) (the dX epilogue then multiplies by a stored value)
+        if mlp_store is None:
+            mlp_store = MLP_STORE_DEFAULT
+        if mlp_store not in ("u", "gd"):
+            raise ValueError(f"mlp_store must be 'u' or 'gd', not {mlp_store!r}")
+        self.mlp_store = mlp_store
         self.res_dtype = torch.bfloat16 if residual == "bf16" else torch.float32
         self.grad_dtype = torch.float32 if residual == "fp32" else torch.bfloat16
         self.blocks = list(model.blocks)
@@ -387,7 +397,9 @@ class FusedGPTEngine:
             xm, h2, mu2, rs2 = ops.add_layernorm_fwd(
                 xs, y, blk.ln_2.weight, blk.ln_2.bias, self.eps, cdt, dropout=state.site(1 + 3 * i)
             )
-            if self.fused_gemm:  # bias + exact-erf GELU in the fc GEMM's epilogue
+            if self.fused_gemm and self.mlp_store == "gd":  # keeps gelu'(u) for the backward (in "u")
+                u, g = ops.linear_fwd_gelu_gd(h2, self._w(blk.mlp_fc.weight), self._w(blk.mlp_fc.bias))
+            elif self.fused_gemm:  # bias + exact-erf GELU in the fc GEMM's epilogue
                 u, g = ops.linear_fwd_gelu(h2, self._w(blk.mlp_fc.weight), self._w(blk.mlp_fc.bias))
             else:
                 u = self._linear(h2, blk.mlp_fc)
@@ -472,7 +484,9 @@ class FusedGPTEngine:
             # MLP: delta = g Wp^T + bp ; dx is d(delta).  Every bias gradient of the block is the
             # column sum of the output gradient its weight-gradient GEMM streams: summed there
             self._wgrad(self._g(blk.mlp_proj.weight), dx_lp, a.g, self._g(blk.mlp_proj.bias))
-            if self.fused_gemm:  # GELU backward in the dX GEMM's epilogue
+            if self.fused_gemm and self.mlp_store == "gd":  # a.u holds gelu'(u): one multiply
+                du = ops.linear_dx_gd(dx_lp, self._w(blk.mlp_proj.weight), a.u)
+            elif self.fused_gemm:  # GELU backward in the dX GEMM's epilogue
                 du = ops.linear_dx_gelu_bwd(dx_lp, self._w(blk.mlp_proj.weight), a.u)
             else:
                 dg = torch.mm(dx_lp, self._w(blk.mlp_proj.weight))

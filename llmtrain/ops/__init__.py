@@ -36,9 +36,11 @@ __all__ = [
     "kernel_policy",
     "layernorm_bwd",
     "linear_dx",
+    "linear_dx_gd",
     "linear_dx_gelu_bwd",
     "linear_fwd",
     "linear_fwd_gelu",
+    "linear_fwd_gelu_gd",
     "ln_param_reduce",
     "policy_state",
     "restore_policy",
@@ -462,6 +464,35 @@ def linear_fwd_gelu(x, w, bias=None):
         return u, g
     u = _lib_mm(x, w.t(), bias, op="fc fwd")
     return u, gelu_fwd(u)
+
+
+def linear_fwd_gelu_gd(x, w, bias=None):
+    """``gd = gelu'(u)`` and ``g = gelu(u)`` of ``u = x @ w^T + bias`` (the bf16 ``u``, as the
+    backward would read it): the fc forward keeps the GELU derivative instead of the
+    pre-activation, so the MLP-projection dX epilogue (:func:`linear_dx_gd`) multiplies by a stored
+    value instead of evaluating erf per element.  GPU: one fused-GEMM epilogue (4) at any size;
+    shapes that kernel does not take form ``u`` on the library and the two maps with torch ops."""
+    if (_on_gpu(x) and x.dtype == torch.bfloat16 and _fgemm_ok_any_size(x, x.shape[1], w.shape[0], w, bias,
+                                                                     op="fc fwd + GELU'")):
+        gd, g = _gemm_rows(x, w, False, 4, bias)
+        return gd, g
+    u = _lib_mm(x, w.t(), bias, op="fc fwd") if _on_gpu(x) else (
+        torch.mm(x, w.t()) if bias is None else torch.addmm(bias, x, w.t()))
+    return ref.gelu_grad(u), gelu_fwd(u)
+
+
+def linear_dx_gd(dy, w, gd, dbias=None):
+    """``du = (dy @ w) * gd`` and ``dbias += colsum(du)`` with ``gd = gelu'(u)`` stored by
+    :func:`linear_fwd_gelu_gd`: the MLP-projection data gradient and the GELU backward in one GEMM
+    epilogue (5) on GPU."""
+    if _on_gpu(dy) and dy.dtype == torch.bfloat16 and _fgemm_ok_any_size(dy, dy.shape[1], w.shape[1], w, gd,
+                                                                         op="MLP-projection dX * gelu'"):
+        return _gemm_rows(dy, w, True, 5, None, gd, dbias)[0]
+    dg = _lib_mm(dy, w, op="MLP-projection dX") if _on_gpu(dy) else torch.mm(dy, w)
+    du = (dg.float() * gd.float()).to(dy.dtype)
+    if dbias is not None:
+        colsum_accum(du, dbias)
+    return du
 
 
 def linear_dx(dy, w):

@@ -33,6 +33,7 @@ __all__ = [
     "embedding_bwd",
     "embedding_fwd",
     "gelu_bwd",
+    "gelu_grad",
     "gelu_fwd",
     "layernorm_bwd",
     "sumsq",
@@ -202,6 +203,14 @@ def gelu_bwd(dg: torch.Tensor, u: torch.Tensor, dbias: torch.Tensor | None) -> t
     if dbias is not None:
         dbias += du.sum(dim=0)
     return du.to(u.dtype)
+
+
+def gelu_grad(u: torch.Tensor) -> torch.Tensor:
+    """``gelu'(u)`` of the exact (erf) GELU, in ``u.dtype`` (computed in fp32)."""
+    uf = u.float()
+    cdf = 0.5 * (1.0 + torch.erf(uf * _INV_SQRT2))
+    pdf = torch.exp(-0.5 * uf * uf) * _INV_SQRT_2PI
+    return (cdf + uf * pdf).to(u.dtype)
 
 
 def colsum_accum(dy: torch.Tensor, out: torch.Tensor) -> None:

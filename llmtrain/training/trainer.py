@@ -197,6 +197,8 @@ class Trainer:
             kw = {}
             if "residual_dtype" in cfg.model.extra:  # fused engine option (gpt_engine.RESIDUAL_MODES)
                 kw["residual"] = str(cfg.model.extra["residual_dtype"])
+            if "mlp_store" in cfg.model.extra:  # fused engine option: "u" | "gd"
+                kw["mlp_store"] = str(cfg.model.extra["mlp_store"])
             engine = model.prepare_runtime(compute_dtype=self._policy.compute_dtype, **kw)
             engine.expect_deterministic = bool(cfg.run.deterministic)
         self._model: nn.Module = model

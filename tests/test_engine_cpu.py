@@ -175,3 +175,21 @@ def test_bf16_residual_streams_track_autograd(residual: str) -> None:
         GPT(**args).prepare_runtime(compute_dtype=torch.float32, residual=residual)
     with pytest.raises(ValueError, match="residual_dtype"):
         GPT(**args).prepare_runtime(compute_dtype=torch.bfloat16, residual="fp16")
+
+
+def test_mlp_store_gd_matches_u() -> None:
+    """model.extra.mlp_store "gd": the fc forward keeps gelu'(u) and the projection dX multiplies
+    by it — the same gradients as keeping u (fp32 reference ops: exactly the same math)."""
+    ref, fused_u = _pair()
+    fused_gd = copy.deepcopy(ref)
+    fused_gd.prepare_runtime(compute_dtype=torch.float32, mlp_store="gd")
+    ids = torch.randint(0, 100, (3, 16))
+    labels = torch.randint(0, 100, (3, 16))
+    for m in (fused_u, fused_gd):
+        m.flat_store.zero_grad()
+        m.fused_loss(ids, labels).backward()
+    for (name, p), (_, q) in zip(fused_gd.named_parameters(), fused_u.named_parameters()):
+        torch.testing.assert_close(p.grad, q.grad, atol=1e-6, rtol=1e-5, msg=name)
+    with pytest.raises(ValueError, match="mlp_store"):
+        GPT(vocab_size=10, block_size=4, d_model=8, n_layers=1, n_heads=2, d_ff=16, dropout=0.0).prepare_runtime(
+            compute_dtype=torch.float32, mlp_store="x")

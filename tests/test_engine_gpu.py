@@ -24,14 +24,14 @@ def _model(dev, **kw):
     return GPT(**args).to(dev)
 
 
-@pytest.mark.parametrize("residual", ["fp32", "bf16_grad", "bf16"])
-def test_fused_matches_module_path(gpu_device, residual):
+@pytest.mark.parametrize("residual,mlp_store", [("fp32", "u"), ("bf16_grad", "u"), ("bf16", "u"), ("bf16", "gd")])
+def test_fused_matches_module_path(gpu_device, residual, mlp_store):
     """bf16 fused path vs fp32 module autograd, for each residual-stream storage option
     (model.extra.residual_dtype): the bf16 forms round the stored residual / gradient values and
     stay inside the same bound."""
     ref_model = _model(gpu_device)
     fused = copy.deepcopy(ref_model)
-    engine = fused.prepare_runtime(compute_dtype=torch.bfloat16, residual=residual)
+    engine = fused.prepare_runtime(compute_dtype=torch.bfloat16, residual=residual, mlp_store=mlp_store)
     ids = torch.randint(0, 1000, (4, 256), device=gpu_device)
     labels = torch.randint(0, 1000, (4, 256), device=gpu_device)
 

@@ -429,6 +429,28 @@ def test_gemm_fused_dgelu(gpu_device, M, N, K, b_kn):
     _close(dbias, 0.5 + du.float().sum(0), 1e-3, 1e-4, "dbias")
 
 
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+@pytest.mark.parametrize("b_kn", [False, True])
+def test_gemm_fused_gelu_and_derivative(gpu_device, M, N, K, b_kn):
+    """Epilogue 4: gelu'(u) and gelu(u) of the bf16 u = a @ w^T + bias (one erf evaluation);
+    epilogue 5: (dy @ W) * stored gelu'(u) with the bias column sums — together equal to
+    epilogue 1 + epilogue 2 up to the bf16 rounding of the stored derivative."""
+    a, w, b, bias = _gemm_operands(M, N, K, b_kn, gpu_device, 9 * M + K)
+    gd, gl = hip().gemm_fused(a, b, b_kn, 4, bias)
+    u, gl1 = hip().gemm_fused(a, b, b_kn, 1, bias)
+    assert torch.equal(gl, gl1)  # the same GELU of the same bf16 u
+    _close(gd, ref.gelu_grad(u.float()), 1e-2, 1e-2, "gelu'(u)")
+    dy, wd, bd, _ = _gemm_operands(M, N, K, not b_kn, gpu_device, 11 * M + N)
+    db5, db2 = torch.zeros(N, device=gpu_device), torch.zeros(N, device=gpu_device)
+    du5, none = hip().gemm_fused(dy, bd, not b_kn, 5, None, gd, db5)
+    assert none is None
+    du2, _ = hip().gemm_fused(dy, bd, not b_kn, 2, None, u, db2)
+    du_ref = (dy.float() @ wd.float().t()) * ref.gelu_grad(u.float()).float()
+    _close(du5, du_ref, 2e-2, 2e-2, "du (stored gelu')")
+    _close(du5, du2, 2e-2, 2e-2, "du: epilogue 5 vs 2")
+    _close(db5, du5.float().sum(0), 1e-3, 1e-4, "dbias sums the written values")
+
+
 @pytest.mark.parametrize(
     "M,N,K,T",
     [(4096, 768, 768, 1024), (1536, 768, 768, 512), (600, 256, 256, 300), (2048, 1600, 1600, 256),

@@ -149,7 +149,7 @@ class _FusedLoss(torch.autograd.Function):
 
 
 RESIDUAL_MODES = ("fp32", "bf16_grad", "bf16")
-MLP_STORE_DEFAULT = "u"
+MLP_STORE_GD_MAX_D = 1024  # default mlp_store "gd" up to this d_model, "u" above
 
 
 class FusedGPTEngine:
@@ -179,14 +179,6 @@ class FusedGPTEngine:
         if residual != "fp32" and compute_dtype != torch.bfloat16:
             raise ValueError("a bf16 residual stream needs the bf16 compute dtype")
         self.residual = residual
-        # what the MLP keeps for its backward (model.extra.mlp_store): "u", the fc pre-activation
-        # (the dX epilogue evaluates gelu'(u)), or "gd", gelu'(u) itself, formed by the fc GEMM's
-        # epilogue from the same erf as gelu(u) (the dX epilogue then multiplies by a stored value)
-        if mlp_store is None:
-            mlp_store = MLP_STORE_DEFAULT
-        if mlp_store not in ("u", "gd"):
-            raise ValueError(f"mlp_store must be 'u' or 'gd', not {mlp_store!r}")
-        self.mlp_store = mlp_store
         self.res_dtype = torch.bfloat16 if residual == "bf16" else torch.float32
         self.grad_dtype = torch.float32 if residual == "fp32" else torch.bfloat16
         self.blocks = list(model.blocks)
@@ -237,6 +229,17 @@ class FusedGPTEngine:
         # MLP projection dX with the GELU backward + fc-bias gradient in its epilogue
         # (LLMTRAIN_FUSED_GEMM=0: hipBLASLt everywhere + separate GELU passes)
         self.fused_gemm = os.environ.get("LLMTRAIN_FUSED_GEMM", "1") != "0"
+        # what the MLP keeps for its backward (model.extra.mlp_store): "u", the fc pre-activation
+        # (the dX epilogue evaluates gelu'(u)), or "gd", gelu'(u) itself, formed by the fc GEMM's
+        # epilogue from the same erf as gelu(u) (the dX epilogue then multiplies by a stored value)
+        if mlp_store is None:
+            # measured (docs/round6.md §8): "gd" +0.5 % at GPT-2 124M (d 768: the fc forward's fused
+            # epilogue costs less than the erf it saves the dX), -0.7 % at GPT-2 XL (d 1600: the
+            # library's fc forward + GELU pass stays ahead of the fused fc forward)
+            mlp_store = "gd" if self.fused_gemm and model.d_model <= MLP_STORE_GD_MAX_D else "u"
+        if mlp_store not in ("u", "gd"):
+            raise ValueError(f"mlp_store must be 'u' or 'gd', not {mlp_store!r}")
+        self.mlp_store = mlp_store
         self.markers = os.environ.get("LLMTRAIN_ROCTX", "0") == "1" and self.store.device.type == "cuda"
         # set by a Trainer with run.deterministic: warn once if a step runs outside its kernel policy
         self.expect_deterministic = False

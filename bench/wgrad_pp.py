@@ -1,7 +1,8 @@
 """Weight-gradient GEMM (csrc/gemm_wgrad_pp.hip): numerics and per-shape timing.
 
     python bench/wgrad_pp.py check            # numerics vs fp32 (every shape, bias, strided dy)
-    python bench/wgrad_pp.py time [--tokens M] [--model gpt2-124m|gpt2-xl|head]
+    python bench/wgrad_pp.py time [--tokens M] [--model gpt2-124m|gpt2-xl|head] [--only pp_slab,pp_slab_square]
+    python bench/wgrad_pp.py sweep2 [--tokens M] [--model ...] [--splits 0,2] [--ssplits 0,4]  # tail tiling
     python bench/wgrad_pp.py sweep [--tokens M] [--model ...] [--splits 1,2,4] [--mode 0]
                                               # fixed split counts (the planner's choice as split 0)
 
@@ -73,7 +74,14 @@ def check() -> int:
     return 1 if bad else 0
 
 
-def time_shapes(model: str, M: int, only: str = "") -> None:
+def _plan(ops, M, N, K, lda, bias, mode):
+    keys = ("swap", "tiles", "split", "chunk", "mode", "nwg", "s_tiles", "s_split", "s_chunk", "s_mode", "s_nwg", "model_ns")
+    return dict(zip(keys, ops.wgrad_pp_plan(M, N, K, lda, K, bias, 0, mode)))
+
+
+def time_shapes(model: str, M: int, only: str = "", rounds: int = 1) -> None:
+    """Time each shape's variants; with ``only`` the variants run in that order, ``rounds`` times
+    (interleaved A/B)."""
     ops = _ops()
     _warm()
     for name, (N, K) in SHAPES[model].items():
@@ -88,13 +96,19 @@ def time_shapes(model: str, M: int, only: str = "") -> None:
             "pp_slab": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, 0),
             "pp_atomic": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, 2),
             "pp_slab_bias": lambda: ops.wgrad_gemm_pp(dy, x, acc, bias, 0, 0),
+            # 256 x 256 tiles only (mode + 8): the rounds-1-5 tiling, A/B of the d = 1600 strips / swap
+            "pp_slab_square": lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, 8),
+            "pp_slab_bias_square": lambda: ops.wgrad_gemm_pp(dy, x, acc, bias, 0, 8),
         }
-        for label, fn in variants.items():
-            if only and label not in only.replace("+", ",").split(","):
-                continue
-            ms = timeit(fn)
-            print(json.dumps({"model": model, "M": M, "gemm": name, "variant": label, "ms": round(ms, 4),
-                              "TFLOPs": round(flops / ms / 1e9, 1)}), flush=True)
+        order = only.replace("+", ",").split(",") if only else list(variants)
+        for mode in (0, 8):
+            print(json.dumps({"model": model, "M": M, "gemm": name, "plan_mode": mode,
+                              **_plan(ops, M, N, K, lda, False, mode)}), flush=True)
+        for _ in range(rounds):
+            for label in order:
+                ms = timeit(variants[label])
+                print(json.dumps({"model": model, "M": M, "gemm": name, "variant": label, "ms": round(ms, 4),
+                                  "TFLOPs": round(flops / ms / 1e9, 1)}), flush=True)
 
 
 def _warm(seconds: float = 1.0) -> None:
@@ -131,6 +145,31 @@ def sweep(model: str, M: int, splits: str, mode: int) -> None:
                               "TFLOPs": round(flops / ms / 1e9, 1)}), flush=True)
 
 
+def sweep2(model: str, M: int, splits: str, ssplits: str, gemms: str = "") -> None:
+    """Time each shape with tail tiling over (main split, strip split) pairs (0 = planned), the
+    256 x 256-only plan first: the data the planner's cost model is checked against."""
+    ops = _ops()
+    _warm()
+    for name, (N, K) in SHAPES[model].items():
+        if gemms and name not in gemms.split(","):
+            continue
+        dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        acc = torch.zeros(N, K, device="cuda")
+        flops = 2.0 * M * N * K
+        timeit(lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, 8))
+        ms = timeit(lambda: ops.wgrad_gemm_pp(dy, x, acc, None, 0, 8))
+        print(json.dumps({"model": model, "M": M, "gemm": name, "square": True, "ms": round(ms, 4),
+                          "TFLOPs": round(flops / ms / 1e9, 1)}), flush=True)
+        for sm in (int(v) for v in splits.split(",")):
+            for ss in (int(v) for v in ssplits.split(",")):
+                sp = sm + 65536 * ss
+                plan = ops.wgrad_pp_plan(M, N, K, N, K, False, sp, 0)
+                ms = timeit(lambda: ops.wgrad_gemm_pp(dy, x, acc, None, sp, 0))
+                print(json.dumps({"model": model, "M": M, "gemm": name, "split": sm, "ssplit": ss, "plan": plan,
+                                  "ms": round(ms, 4), "TFLOPs": round(flops / ms / 1e9, 1)}), flush=True)
+
+
 def one(gemm: str, variant: str, M: int, reps: int) -> None:
     """Run one shape / kernel ``reps`` times (a target for rocprofv3 counter passes)."""
     ops = _ops()
@@ -147,26 +186,31 @@ def one(gemm: str, variant: str, M: int, reps: int) -> None:
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["check", "time", "one", "sweep"])
+    ap.add_argument("what", choices=["check", "time", "one", "sweep", "sweep2"])
     ap.add_argument("--gemm", default="qkv")
     ap.add_argument("--variant", default="pp")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default="", help="comma-separated variant labels (time)")
     ap.add_argument("--tokens", type=int, default=131072)
+    ap.add_argument("--rounds", type=int, default=1, help="time: repeat the variant sequence")
     ap.add_argument("--model", default="gpt2-124m", choices=sorted(SHAPES))
     ap.add_argument("--splits", default="0,1,2,3,4,5,6,8")
+    ap.add_argument("--ssplits", default="0,1,2,4,8,16,32", help="sweep2: strip splits")
     ap.add_argument("--mode", type=int, default=0,
                     help="sweep: 0 slabs + finishing launch, 2 atomics, -1 auto")
     args = ap.parse_args()
     if args.what == "check":
         return check()
+    if args.what == "sweep2":
+        sweep2(args.model, args.tokens, args.splits, args.ssplits, args.gemm if args.gemm != "qkv" or "--gemm" in sys.argv else "")
+        return 0
     if args.what == "sweep":
         sweep(args.model, args.tokens, args.splits, args.mode)
         return 0
     if args.what == "one":
         one(args.gemm, args.variant, args.tokens, args.reps)
         return 0
-    time_shapes(args.model, args.tokens, args.only)
+    time_shapes(args.model, args.tokens, args.only, args.rounds)
     return 0
 
 

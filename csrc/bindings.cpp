@@ -520,6 +520,15 @@ void wgrad_gemm_pp(const Tensor& dy, const Tensor& x, Tensor c, const c10::optio
             "wgrad_gemm_pp");
 }
 
+// the weight-gradient plan for a shape (introspection for tests and bench/wgrad_pp.py; no GPU work)
+std::vector<int64_t> wgrad_pp_plan(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, bool bias, int64_t split,
+                                   int64_t mode) {
+  long out[12] = {0};
+  const int n = llmt::wgrad_pp_plan_info((int)lda, (int)ldb, (int)M, (int)N, (int)K, bias, (int)split, (int)mode, out);
+  TORCH_CHECK(n == 12, "wgrad_pp_plan: invalid shape");
+  return std::vector<int64_t>(out, out + 12);
+}
+
 // ---- fused forward / dX GEMM ------------------------------------------------------------------
 // out = epi(a @ op(b)): b is [N, K] (weight, forward) or, with b_kn, [K, N] (weight in dX = dy @ W).
 // epilogue 0 -> (out, None); 1 -> (u, gelu(u)); 2 -> (du = acc * gelu'(u), None) with dbias += colsum.
@@ -737,6 +746,8 @@ TORCH_LIBRARY(llmtrain_hip, m) {
   m.def("get_deterministic() -> bool", &get_deterministic);
   m.def("set_dropout_seed_offset(Tensor? word) -> ()", &set_dropout_seed_offset);
   m.def("wgrad_gemm_pp(Tensor dy, Tensor x, Tensor(a!) c, Tensor(b!)? bias=None, int split=0, int mode=-1) -> ()");
+  m.def("wgrad_pp_plan(int M, int N, int K, int lda, int ldb, bool bias, int split=0, int mode=-1) -> int[]",
+        &wgrad_pp_plan);  // catch-all: no tensor arguments
   m.def("gemm_fused(Tensor a, Tensor b, bool b_kn, int epilogue, Tensor? bias=None, Tensor? u=None,"
         " Tensor(a!)? dbias=None, int seq_len=0, Tensor(b!)? out=None) -> (Tensor, Tensor?)");
   m.def("sumsq(Tensor x) -> Tensor");

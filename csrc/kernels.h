@@ -153,8 +153,13 @@ hipError_t launch_clip_coef(const float* sumsq, float max_norm, float* out, hipS
 
 // Ping-pong weight-gradient GEMM (gemm_wgrad_pp.hip): C[N,K] += dy^T x and, with `bias`,
 // bias[N] += colsum(dy).  `ws` holds wgrad_pp_ws_floats(...) floats (split slabs + bias parts).
-// mode: -1 auto, 0 slabs + fixed-order reduce, 2 fp32 atomics (ignored in deterministic mode).
+// mode: -1 auto, 0 slabs + fixed-order reduce, 2 fp32 atomics (ignored in deterministic mode);
+// mode + 8 (7, 8, 10): 256 x 256 tiles only, without the K-tail strips / operand swap (A/B timing).
+// split: 0 planned; else the 256 x 256 tiles' split + 65536 x the strips' split (0 = planned).
 long wgrad_pp_ws_floats(int lda, int ldb, int M, int N, int K, int split, int mode, bool bias);
+// the plan launch_wgrad_pp takes: {swap, then per family (256x256, strips): tiles, split, rows per
+// chunk, epilogue mode, workgroups; modelled ns}; returns the count written (12) or 0
+int wgrad_pp_plan_info(int lda, int ldb, int M, int N, int K, bool bias, int split, int mode, long* out);
 hipError_t launch_wgrad_pp(const void* dy, int lda, const void* x, int ldb, float* c, int ldc, int M, int N, int K,
                            int split, int mode, float* ws, float* bias, hipStream_t stream);
 // ---- forward / data-gradient GEMM with fused epilogues (bf16 in, fp32 accumulate, bf16 out)

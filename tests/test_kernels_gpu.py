@@ -329,12 +329,18 @@ def test_layernorm_bwd_deferred_params_batched(gpu_device, M, d):
 @pytest.mark.parametrize("M,N,K,lda", [(4096, 768, 768, 768), (2048, 2304, 768, 2304), (1000, 200, 72, 200),
                                         (3000, 1000, 768, 1024), (2080, 1600, 4800, 1600),
                                         (1500, 1001, 768, 1024), (101, 768, 768, 768),
-                                        (2048, 50257, 768, 50304)])  # the LM head's padded logits
+                                        (2048, 50257, 768, 50304),  # the LM head's padded logits
+                                        # K tails of 64 / 128 columns -> 512 x 64 strip tiles
+                                        (2048, 1600, 1600, 1600), (3000, 6400, 1600, 6400), (101, 1600, 1600, 1600),
+                                        (1200, 512, 640, 512),
+                                        # N tail, whole K -> swapped operands, transposed output
+                                        (2500, 1600, 6400, 1600), (1500, 320, 2304, 320),
+                                        (1500, 320, 2304, 384)])  # lda > N: bias call unswapped, split=3 call swapped
 def test_wgrad_gemm_pp(gpu_device, M, N, K, lda, mode):
     """Ping-pong weight-gradient GEMM (csrc/gemm_wgrad_pp.hip): dst += dY^T X and bias += colsum(dY)
     against fp32, for the auto plan, the slab (deterministic) and the atomic epilogue, ragged M/N/K,
     a column-slice dY (row stride lda > N), a single-stage chunk and an odd stage count (the
-    zero-padded last stage)."""
+    zero-padded last stage), the K-tail strip tiles and the swapped (transposed-output) plan."""
     g = torch.Generator(device="cpu").manual_seed(M + N + K + mode)
     dy = torch.randn(M, lda, generator=g).to(gpu_device, torch.bfloat16)[:, :N]
     x = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)
@@ -351,20 +357,39 @@ def test_wgrad_gemm_pp(gpu_device, M, N, K, lda, mode):
     _close(c2, dy.float().t() @ x.float(), 2e-5 * want.abs().max().item(), 1e-4, "wgrad_pp split=3")
 
 
-def test_wgrad_gemm_pp_slabs_bitwise(gpu_device):
+@pytest.mark.parametrize("N,K", [(2304, 768), (6400, 1600), (1600, 6400)])
+def test_wgrad_gemm_pp_slabs_bitwise(gpu_device, N, K):
     """The slab epilogue reduces the split partials in a fixed order: repeated launches are equal
-    bit for bit (the deterministic mode needs no separate path)."""
+    bit for bit (the deterministic mode needs no separate path) — also with strip tiles (6400 x
+    1600) and the swapped plan with its separate bias pass (1600 x 6400)."""
     g = torch.Generator(device="cpu").manual_seed(5)
-    dy = torch.randn(16384, 2304, generator=g).to(gpu_device, torch.bfloat16)
-    x = torch.randn(16384, 768, generator=g).to(gpu_device, torch.bfloat16)
+    dy = torch.randn(16384, N, generator=g).to(gpu_device, torch.bfloat16)
+    x = torch.randn(16384, K, generator=g).to(gpu_device, torch.bfloat16)
     outs = []
     for _ in range(3):
-        c = torch.zeros(2304, 768, device=gpu_device)
-        b = torch.zeros(2304, device=gpu_device)
+        c = torch.zeros(N, K, device=gpu_device)
+        b = torch.zeros(N, device=gpu_device)
         hip().wgrad_gemm_pp(dy, x, c, b, 0, 0)
         outs.append((c, b))
     for c, b in outs[1:]:
         assert torch.equal(c, outs[0][0]) and torch.equal(b, outs[0][1])
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 1600, 1600), (4096, 4800, 1600), (4096, 1600, 6400)])
+def test_wgrad_gemm_pp_tail_tiling_vs_square_tiles(gpu_device, M, N, K):
+    """The d = 1600 tilings (strips / swapped operands) against the 256 x 256-only plan (mode + 8)
+    and fp32: both within the same bound of the fp32 product, bias included."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    dy = torch.randn(M, N, generator=g).to(gpu_device, torch.bfloat16)
+    x = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)
+    want = dy.float().t() @ x.float()
+    want_b = dy.float().sum(0)
+    for mode in (0, 8):
+        c = torch.zeros(N, K, device=gpu_device)
+        b = torch.zeros(N, device=gpu_device)
+        hip().wgrad_gemm_pp(dy, x, c, b, 0, mode)
+        _close(c, want, 2e-5 * want.abs().max().item(), 1e-4, f"wgrad_pp mode {mode}")
+        _close(b, want_b, 2e-5 * want_b.abs().max().item(), 1e-4, f"wgrad_pp bias mode {mode}")
 
 
 # ---- fused forward / dX GEMM (csrc/gemm_fused.hip) -------------------------------------------

@@ -196,13 +196,14 @@ def main() -> int:
     ap.add_argument("--model", default="gpt2-124m", choices=sorted(SHAPES))
     ap.add_argument("--splits", default="0,1,2,3,4,5,6,8")
     ap.add_argument("--ssplits", default="0,1,2,4,8,16,32", help="sweep2: strip splits")
+    ap.add_argument("--gemms", default="", help="sweep2: comma-separated shape names (default all)")
     ap.add_argument("--mode", type=int, default=0,
                     help="sweep: 0 slabs + finishing launch, 2 atomics, -1 auto")
     args = ap.parse_args()
     if args.what == "check":
         return check()
     if args.what == "sweep2":
-        sweep2(args.model, args.tokens, args.splits, args.ssplits, args.gemm if args.gemm != "qkv" or "--gemm" in sys.argv else "")
+        sweep2(args.model, args.tokens, args.splits, args.ssplits, args.gemms)
         return 0
     if args.what == "sweep":
         sweep(args.model, args.tokens, args.splits, args.mode)

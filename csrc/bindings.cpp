@@ -348,7 +348,9 @@ void embedding_bwd(const Tensor& dx, const Tensor& ids, Tensor dwte, Tensor dwpe
   check_gpu(ids, "ids");
   check_gpu(dwte, "dwte");
   check_gpu(dwpe, "dwpe");
-  check_dtype(dx, at::kFloat, "dx");
+  TORCH_CHECK(dx.scalar_type() == at::kFloat || dx.scalar_type() == at::kBFloat16, "dx must be float32 or bfloat16");
+  TORCH_CHECK(dx.is_contiguous(), "dx must be contiguous");
+  const bool dx_bf16 = dx.scalar_type() == at::kBFloat16;
   check_dtype(ids, at::kLong, "ids");
   check_dtype(dwte, at::kFloat, "dwte");
   check_dtype(dwpe, at::kFloat, "dwpe");
@@ -357,7 +359,7 @@ void embedding_bwd(const Tensor& dx, const Tensor& ids, Tensor dwte, Tensor dwpe
   at::hip::HIPGuardMasqueradingAsCUDA guard(dx.device());
   if (B * T == 0) return;
   const llmt::DropoutArgs dr = make_dropout(dropout_p, dropout_seed);
-  check_hip(llmt::launch_embedding_bwd(dx.data_ptr<float>(), ids.data_ptr<int64_t>(),
+  check_hip(llmt::launch_embedding_bwd(dx.data_ptr(), dx_bf16, ids.data_ptr<int64_t>(),
                                        llmt::deterministic() ? nullptr : dwte.data_ptr<float>(),
                                        dwpe.data_ptr<float>(), (int)B, (int)T, (int)d, (int)dwte.size(0), dr,
                                        cur_stream()),
@@ -368,7 +370,7 @@ void embedding_bwd(const Tensor& dx, const Tensor& ids, Tensor dwte, Tensor dwpe
     auto sorted = ids.reshape({-1}).sort(/*stable=*/true, /*dim=*/0, /*descending=*/false);
     const Tensor& sorted_ids = std::get<0>(sorted);
     const Tensor& order = std::get<1>(sorted);
-    check_hip(llmt::launch_embedding_bwd_sorted(dx.data_ptr<float>(), sorted_ids.data_ptr<int64_t>(),
+    check_hip(llmt::launch_embedding_bwd_sorted(dx.data_ptr(), dx_bf16, sorted_ids.data_ptr<int64_t>(),
                                                 order.data_ptr<int64_t>(), dwte.data_ptr<float>(), (int)(B * T),
                                                 (int)d, (int)dwte.size(0), dr, cur_stream()),
               "embedding_bwd_sorted");

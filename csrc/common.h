@@ -51,6 +51,15 @@ __device__ __forceinline__ bf16_raw f2bf(float f) {
   return __builtin_bit_cast(bf16_raw, b);
 }
 
+// one element / four consecutive elements of an fp32 or bf16 stream, as fp32
+__device__ __forceinline__ float to_f32(float v) { return v; }
+__device__ __forceinline__ float to_f32(bf16_raw v) { return bf2f(v); }
+__device__ __forceinline__ float4_t load4_f32(const float* p) { return *reinterpret_cast<const float4_t*>(p); }
+__device__ __forceinline__ float4_t load4_f32(const bf16_raw* p) {
+  const ushort4_t v = *reinterpret_cast<const ushort4_t*>(p);
+  return float4_t{bf2f(v[0]), bf2f(v[1]), bf2f(v[2]), bf2f(v[3])};
+}
+
 // 8 x bf16 <-> 8 x f32
 __device__ __forceinline__ void unpack8(const ushort8_t v, float* f) {
 #pragma unroll

@@ -5,6 +5,8 @@
 // Reference call sites: models/gpt.py:94-95/:102-103 (nn.GELU, exact erf), :176-179 (token and
 // position embeddings; gradient of the tied [V, d] table), Linear bias gradients.
 
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -209,8 +211,10 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __res
 }
 
 // dwte[ids[row]] += dx[row]: each wave adds one contiguous row (256-B wave segments, the
-// full-rate atomic shape on MI355X).
-__global__ __launch_bounds__(256) void embedding_bwd_tok_kernel(const float* __restrict__ dx,
+// full-rate atomic shape on MI355X).  dx is the residual-stream gradient, fp32 or bf16 (read as is:
+// no widening pass).
+template <typename TX>
+__global__ __launch_bounds__(256) void embedding_bwd_tok_kernel(const TX* __restrict__ dx,
                                                                 const int64_t* __restrict__ ids,
                                                                 float* __restrict__ dwte, int M,
                                                                 int d, int V, DropoutArgs dr) {
@@ -221,17 +225,18 @@ __global__ __launch_bounds__(256) void embedding_bwd_tok_kernel(const float* __r
   const long tok = ids[row];
   LLMT_DASSERT(tok >= 0 && tok < V);
   if (tok < 0 || tok >= V) return;
-  const float* src = dx + row * (long)d;
+  const TX* src = dx + row * (long)d;
   float* dst = dwte + tok * (long)d;
   for (int c = lane; c < d; c += 64) {
-    float g = src[c];
+    float g = to_f32(src[c]);
     if (dr.thr != 0) g = drop_keep(dr.seed, dr.thr, (uint64_t)row * d + c) ? g * dr.scale : 0.f;
     atomicAdd(dst + c, g);
   }
 }
 
-// dwpe[t] += sum_b dx[b, t]: one thread per (t, float4 column chunk), no atomics.
-__global__ __launch_bounds__(256) void embedding_bwd_pos_kernel(const float* __restrict__ dx,
+// dwpe[t] += sum_b dx[b, t]: one thread per (t, 4-column chunk), no atomics.
+template <typename TX>
+__global__ __launch_bounds__(256) void embedding_bwd_pos_kernel(const TX* __restrict__ dx,
                                                                 float* __restrict__ dwpe, int B,
                                                                 int T, int d, DropoutArgs dr) {
   resolve_dropout(dr);
@@ -242,7 +247,7 @@ __global__ __launch_bounds__(256) void embedding_bwd_pos_kernel(const float* __r
   float4_t acc = {0.f, 0.f, 0.f, 0.f};
   for (int b = 0; b < B; ++b) {
     const long row = (long)b * T + t;
-    float4_t g = reinterpret_cast<const float4_t*>(dx + row * d)[c];
+    float4_t g = load4_f32(dx + row * d + 4 * c);
     if (dr.thr != 0) {
       const uint64_t e0 = (uint64_t)row * d + 4 * c;
 #pragma unroll
@@ -330,16 +335,21 @@ hipError_t launch_embedding_fwd(const int64_t* ids, const float* wte, const floa
   return hipGetLastError();
 }
 
-hipError_t launch_embedding_bwd(const float* dx, const int64_t* ids, float* dwte, float* dwpe, int B, int T,
-                                int d, int V, DropoutArgs dropout, hipStream_t stream) {
+hipError_t launch_embedding_bwd(const void* dx, bool dx_bf16, const int64_t* ids, float* dwte, float* dwpe, int B,
+                                int T, int d, int V, DropoutArgs dropout, hipStream_t stream) {
   if (d % 4 != 0) return hipErrorInvalidValue;
   const int M = B * T;
-  if (dwte != nullptr)  // nullptr: the caller scatters the token gradient itself (deterministic mode)
-    hipLaunchKernelGGL(embedding_bwd_tok_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, dx, ids, dwte, M, d, V,
-                       dropout);
   const long work = (long)T * (d / 4);
-  hipLaunchKernelGGL(embedding_bwd_pos_kernel, dim3((work + 255) / 256), dim3(256), 0, stream, dx, dwpe, B, T, d,
-                     dropout);
+  auto run = [&](auto* x) {
+    using TX = std::remove_const_t<std::remove_pointer_t<decltype(x)>>;
+    if (dwte != nullptr)  // nullptr: the caller scatters the token gradient itself (deterministic mode)
+      hipLaunchKernelGGL(embedding_bwd_tok_kernel<TX>, dim3((M + 3) / 4), dim3(256), 0, stream, x, ids, dwte, M, d,
+                         V, dropout);
+    hipLaunchKernelGGL(embedding_bwd_pos_kernel<TX>, dim3((work + 255) / 256), dim3(256), 0, stream, x, dwpe, B, T,
+                       d, dropout);
+  };
+  if (dx_bf16) run(static_cast<const bf16_raw*>(dx));
+  else run(static_cast<const float*>(dx));
   return hipGetLastError();
 }
 

@@ -94,7 +94,8 @@ hipError_t launch_colsum_accum(const void* dy, bool bf16, float* out, float* ws,
 // x = dropout(wte[ids] + wpe[t]); the backward applies the same mask to dx before the scatter
 hipError_t launch_embedding_fwd(const int64_t* ids, const float* wte, const float* wpe, void* x, bool x_bf16,
                                 int B, int T, int d, int V, DropoutArgs dropout, hipStream_t stream);
-hipError_t launch_embedding_bwd(const float* dx, const int64_t* ids, float* dwte, float* dwpe,
+// dx: the residual-stream gradient [B*T, d], fp32 or (dx_bf16) bf16
+hipError_t launch_embedding_bwd(const void* dx, bool dx_bf16, const int64_t* ids, float* dwte, float* dwpe,
                                 int B, int T, int d, int V, DropoutArgs dropout, hipStream_t stream);
 // keep-mask of elements 0..n-1 of one dropout site (tests)
 hipError_t launch_dropout_mask(DropoutArgs dropout, bool* out, long long n, hipStream_t stream);
@@ -118,8 +119,8 @@ void set_deterministic(bool on);
 bool deterministic();
 // dwte[v] += sum of dx[order[j]] over the run of sorted_ids == v (stable sort of the tokens):
 // one writer per row, fixed order — the deterministic form of launch_embedding_bwd's scatter.
-hipError_t launch_embedding_bwd_sorted(const float* dx, const int64_t* sorted_ids, const int64_t* order, float* dwte,
-                                       int M, int d, int V, DropoutArgs dropout, hipStream_t stream);
+hipError_t launch_embedding_bwd_sorted(const void* dx, bool dx_bf16, const int64_t* sorted_ids, const int64_t* order,
+                                       float* dwte, int M, int d, int V, DropoutArgs dropout, hipStream_t stream);
 
 // ---- optimizer ---------------------------------------------------------------------------
 struct AdamWArgs {

@@ -94,7 +94,8 @@ __global__ __launch_bounds__(64 * kWaves) void colsum_parts_kernel(Jobs jobs, in
 int num_groups(int nparts) { return nparts <= kOneLevel ? 1 : (nparts + kGroup - 1) / kGroup; }
 
 // rows [i0, i1) of the sorted order with equal tokens: the wave at a run's first row sums it
-__global__ __launch_bounds__(256) void embedding_bwd_sorted_kernel(const float* __restrict__ dx,
+template <typename TX>
+__global__ __launch_bounds__(256) void embedding_bwd_sorted_kernel(const TX* __restrict__ dx,
                                                                    const int64_t* __restrict__ sorted_ids,
                                                                    const int64_t* __restrict__ order,
                                                                    float* __restrict__ dwte, int M, int d, int V,
@@ -111,12 +112,12 @@ __global__ __launch_bounds__(256) void embedding_bwd_sorted_kernel(const float* 
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     for (long j = i; j < M && sorted_ids[j] == tok; ++j) {
       const long row = order[j];
-      const float* src = dx + row * (long)d;
+      const TX* src = dx + row * (long)d;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int c = c0 + lane + 64 * k;
         if (c < d) {
-          float g = src[c];
+          float g = to_f32(src[c]);
           if (dr.thr != 0) g = drop_keep(dr.seed, dr.thr, (uint64_t)row * d + c) ? g * dr.scale : 0.f;
           acc[k] += g;
         }
@@ -179,11 +180,15 @@ hipError_t launch_colsum_reduce(const float* parts, int nparts, long ncols, floa
   return launch_colsum_reduce_multi(&parts, &dst, 1, nparts, ncols, scratch, stream, row_len, dst_ld);
 }
 
-hipError_t launch_embedding_bwd_sorted(const float* dx, const int64_t* sorted_ids, const int64_t* order, float* dwte,
-                                       int M, int d, int V, DropoutArgs dropout, hipStream_t stream) {
+hipError_t launch_embedding_bwd_sorted(const void* dx, bool dx_bf16, const int64_t* sorted_ids, const int64_t* order,
+                                       float* dwte, int M, int d, int V, DropoutArgs dropout, hipStream_t stream) {
   if (M <= 0) return hipSuccess;
-  hipLaunchKernelGGL(embedding_bwd_sorted_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, dx, sorted_ids, order, dwte,
-                     M, d, V, dropout);
+  if (dx_bf16)
+    hipLaunchKernelGGL(embedding_bwd_sorted_kernel<bf16_raw>, dim3((M + 3) / 4), dim3(256), 0, stream,
+                       static_cast<const bf16_raw*>(dx), sorted_ids, order, dwte, M, d, V, dropout);
+  else
+    hipLaunchKernelGGL(embedding_bwd_sorted_kernel<float>, dim3((M + 3) / 4), dim3(256), 0, stream,
+                       static_cast<const float*>(dx), sorted_ids, order, dwte, M, d, V, dropout);
   return hipGetLastError();
 }
 

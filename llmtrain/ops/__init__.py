@@ -248,11 +248,11 @@ def embedding_fwd(ids, wte, wpe, dropout=(0.0, 0), out_dtype=torch.float32):
 
 
 def embedding_bwd(dx, ids, dwte, dwpe, dropout=(0.0, 0)) -> None:
-    """Token / position embedding gradients from the residual-stream gradient ``dx`` (a bf16
-    gradient stream is widened once here: the scatter kernels read fp32 rows)."""
+    """Token / position embedding gradients from the residual-stream gradient ``dx`` (fp32 or
+    bf16: the scatter kernels read either stream as is)."""
     p, seed = dropout
     if _on_gpu(dx):
-        hip_ops().embedding_bwd(dx.float(), ids, dwte, dwpe, p, seed)
+        hip_ops().embedding_bwd(dx.contiguous(), ids, dwte, dwpe, p, seed)
     else:
         ref.embedding_bwd(dx, ids, dwte, dwpe, p, seed)
 

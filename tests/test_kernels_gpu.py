@@ -179,6 +179,28 @@ def test_embedding(gpu_device):
     _close(dwpe, dwpe_r, 1e-4, 1e-5, "dwpe")
 
 
+@pytest.mark.parametrize("det", [False, True])
+def test_embedding_bwd_bf16_stream(gpu_device, det):
+    """The embedding backward reads a bf16 residual-stream gradient as is (atomic scatter and the
+    deterministic sorted scatter): equal to the fp32 oracle on the same bf16 values."""
+    g = torch.Generator(device="cpu").manual_seed(15)
+    B, T, d, V = 4, 128, 768, 3000
+    ids = torch.randint(0, V, (B, T), generator=g).to(gpu_device)
+    ids[1, :20] = 11
+    dx = torch.randn(B * T, d, generator=g).to(gpu_device, torch.bfloat16)
+    dwte, dwpe = torch.zeros(V, d, device=gpu_device), torch.zeros(256, d, device=gpu_device)
+    dwte_r, dwpe_r = dwte.clone(), dwpe.clone()
+    prev = hip().get_deterministic()
+    hip().set_deterministic(det)
+    try:
+        hip().embedding_bwd(dx, ids, dwte, dwpe)
+    finally:
+        hip().set_deterministic(prev)
+    ref.embedding_bwd(dx.float(), ids, dwte_r, dwpe_r)
+    _close(dwte, dwte_r, 1e-4, 1e-5, "dwte bf16 dx")
+    _close(dwpe, dwpe_r, 1e-4, 1e-5, "dwpe bf16 dx")
+
+
 def test_sumsq_and_adamw(gpu_device):
     g = torch.Generator(device="cpu").manual_seed(6)
     n = 1_000_003  # ragged tail

@@ -93,7 +93,10 @@ struct Geo {
   static constexpr int OPSB = (4 * ROWB + 1023) / 1024;
   static constexpr int NOPS = OPSA + OPSB;
 };
-constexpr int kSmemBytes = 2 * Geo<true>::SLOT;  // 72 KiB: two ring slots of the larger geometry
+constexpr int kSmemBytes = 2 * Geo<true>::SLOT;
+#ifndef LLMT_WPP_L2_PROBE
+#define LLMT_WPP_L2_PROBE 0  // 1: variant build whose operand loads stay L2-resident (timing probe)
+#endif  // 72 KiB: two ring slots of the larger geometry
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -221,7 +224,11 @@ __device__ __forceinline__ void tile_body(const Args& p, const Seg& sg, int w, u
   // (unconditional: a stage past the chunk has a zero-record descriptor and loads zeros — a
   // conditional load made hipcc drain every outstanding load before each LDS write)
   auto load_stage = [&](int st, u32x4 (&R)[G::NOPS]) {
+#if LLMT_WPP_L2_PROBE
+    const int r0 = (st & 1) * BR, nr = max(0, min(BR, rows - r0));  // timing probe: the chunk's first two stages again (L2-hot, wrong results)
+#else
     const int r0 = st * BR, nr = max(0, min(BR, rows - r0));
+#endif
     const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(p.A + (long)(m_begin + r0) * p.lda, nr * p.lda * 2);
     const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(p.B + (long)(m_begin + r0) * p.ldb, nr * p.ldb * 2);
 #pragma unroll

@@ -225,7 +225,8 @@ __device__ __forceinline__ void tile_body(const Args& p, const Seg& sg, int w, u
   // conditional load made hipcc drain every outstanding load before each LDS write)
   auto load_stage = [&](int st, u32x4 (&R)[G::NOPS]) {
 #if LLMT_WPP_L2_PROBE
-    const int r0 = (st & 1) * BR, nr = max(0, min(BR, rows - r0));  // timing probe: the chunk's first two stages again (L2-hot, wrong results)
+    // timing probe: the chunk's first two stages again (L2-hot, wrong results)
+    const int r0 = (st & 1) * BR, nr = max(0, min(BR, rows - r0));
 #else
     const int r0 = st * BR, nr = max(0, min(BR, rows - r0));
 #endif

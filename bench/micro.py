@@ -189,31 +189,39 @@ def head_ce(M: int = 131072) -> None:
             print(json.dumps({"head_ce": name, "M": M, "ms": round(ms, 3), "same_loss_rows": same}), flush=True)
 
 
-def ln(M: int = 65536, d: int = 768) -> None:
-    """LayerNorm forward (+residual add) and backward at the engine's call shapes; GB/s moved."""
+def ln(M: int = 65536, d: int = 768, res: str = "bf16") -> None:
+    """LayerNorm forward (+residual add) and backward at the engine's call shapes; GB/s moved.
+    ``res``: residual stream and its gradient in bf16 (the engine's default with bf16 compute) or
+    fp32."""
     from llmtrain.ops import _ext
 
     _ext.require()
     ops = torch.ops.llmtrain_hip
     dev = torch.device("cuda")
-    x = torch.randn(M, d, device=dev)
+    rdt = torch.bfloat16 if res == "bf16" else torch.float32
+    rb = 2 if res == "bf16" else 4
+    x = torch.randn(M, d, device=dev, dtype=rdt)
     delta = torch.randn(M, d, device=dev, dtype=torch.bfloat16)
     w = torch.ones(d, device=dev)
     b = torch.zeros(d, device=dev)
     xs, h, mu, rs = ops.add_layernorm_fwd(x, delta, w, b, 1e-5, torch.bfloat16)
     ms = timeit(lambda: ops.add_layernorm_fwd(x, delta, w, b, 1e-5, torch.bfloat16))
-    gb = M * d * (4 + 2 + 4 + 2) / 1e9
-    print(json.dumps({"op": "add_ln_fwd", "ms": round(ms, 4), "GB/s": round(gb / ms * 1e3, 1)}), flush=True)
+    gb = M * d * (rb + 2 + rb + 2) / 1e9
+    print(json.dumps({"op": "add_ln_fwd", "M": M, "d": d, "res": res, "ms": round(ms, 4),
+                      "GB/s": round(gb / ms * 1e3, 1)}), flush=True)
     dy = torch.randn(M, d, device=dev, dtype=torch.bfloat16)
-    dres = torch.randn(M, d, device=dev)
+    dres = torch.randn(M, d, device=dev, dtype=rdt)
     dw, db, dp = (torch.zeros(d, device=dev) for _ in range(3))
-    ms = timeit(lambda: ops.layernorm_bwd(dy, xs, mu, rs, w, dres, dw, db, None, True, dp))
-    gb = M * d * (2 + 4 + 4 + 4 + 2) / 1e9
-    print(json.dumps({"op": "ln_bwd", "ms": round(ms, 4), "GB/s": round(gb / ms * 1e3, 1)}), flush=True)
+    lowp = res == "bf16"
+    ms = timeit(lambda: ops.layernorm_bwd(dy, xs, mu, rs, w, dres, dw, db, None, True, dp, 0.0, 0, lowp))
+    gb = M * d * (2 + rb + rb + rb) / 1e9
+    print(json.dumps({"op": "ln_bwd", "M": M, "d": d, "res": res, "ms": round(ms, 4),
+                      "GB/s": round(gb / ms * 1e3, 1)}), flush=True)
     u = torch.randn(M, 4 * d, device=dev, dtype=torch.bfloat16)
     ms = timeit(lambda: ops.gelu_fwd(u))
     gb = M * 4 * d * 4 / 1e9
-    print(json.dumps({"op": "gelu_fwd", "ms": round(ms, 4), "GB/s": round(gb / ms * 1e3, 1)}), flush=True)
+    print(json.dumps({"op": "gelu_fwd", "M": M, "d": d, "ms": round(ms, 4), "GB/s": round(gb / ms * 1e3, 1)}),
+          flush=True)
 
 
 def attn(B: int = 32, T: int = 1024, H: int = 12, sdpa: bool = True) -> list[dict]:
@@ -266,7 +274,8 @@ if __name__ == "__main__":
     if what == "fwd":  # forward / dX GEMMs
         gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 65536, only="fwd")
     if what == "ln":
-        ln(int(sys.argv[2]) if len(sys.argv) > 2 else 65536)
+        ln(int(sys.argv[2]) if len(sys.argv) > 2 else 65536, int(sys.argv[3]) if len(sys.argv) > 3 else 768,
+           sys.argv[4] if len(sys.argv) > 4 else "bf16")
     if what == "fgemm1":  # K N epi b_kn
         fgemm_one(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5] == "1",
                   M=int(sys.argv[6]) if len(sys.argv) > 6 else 65536)

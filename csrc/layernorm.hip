@@ -49,80 +49,102 @@ __device__ __forceinline__ float4_t round_bf16x4(float4_t v) {
   return float4_t{bf2f(f2bf(v[0])), bf2f(f2bf(v[1])), bf2f(f2bf(v[2])), bf2f(f2bf(v[3]))};
 }
 
-constexpr int kLnWaves = 4;  // rows per workgroup in the forward
+constexpr int kLnWaves = 4;  // rows per workgroup in the forward (per resident wave, persistent)
 
 // MAXC = max float4 chunks per lane = ceil(d / 4 / 64); TX = storage type of the residual stream
 // (x in, x + delta out): float, or bf16 for the engine's bf16 residual option, in which case the
 // sum is rounded to bf16 BEFORE the statistics, so the backward's x-hat of the stored value is the
 // forward's exactly (the add and the statistics themselves stay fp32 in registers)
+// Rows wider than 768 columns (MAXC > 3, GPT-2 XL's d = 1600) run persistent: each wave loads
+// gamma / beta once and strides over rows (M = 32768, d = 1600: 0.087 vs 0.097 ms; at d = 768 the
+// one-row-per-wave launch stays ahead, 0.151 vs 0.159 ms; profiles/r6/ln/).
+template <int MAXC>
+constexpr bool ln_fwd_persistent() { return MAXC > 3; }
+
 template <int MAXC, typename TD, typename TY, typename TX>
 __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
     const TX* __restrict__ x, const TD* __restrict__ delta, const float* __restrict__ w,
     const float* __restrict__ b, TX* __restrict__ xs_out, TY* __restrict__ y,
     float* __restrict__ mean_out, float* __restrict__ rstd_out, int M, int d, float eps, DropoutArgs dr) {
   resolve_dropout(dr);
+  constexpr bool kPersist = ln_fwd_persistent<MAXC>();
   const int lane = threadIdx.x & 63;
-  const long row = (long)blockIdx.x * kLnWaves + (threadIdx.x >> 6);
-  if (row >= M) return;
   const int nc = d >> 2;
-  const TX* xr = x + row * d;
-  // unconditional loads (lanes past the row end read column 0 and are zeroed): a load under a
-  // divergent `if` gets a vmcnt(0) at the branch join, one HBM round trip per 256-column chunk
-  // gamma / beta are loaded with the row (on gfx950 vmcnt also counts stores: loading them after
-  // the xs stores would wait for those stores to complete)
-  float4_t v[MAXC], dv[MAXC], ww[MAXC], bb[MAXC];
-#pragma unroll
-  for (int j = 0; j < MAXC; ++j) {
-    const int c = lane + j * 64, cc = c < nc ? c : 0;
-    v[j] = load4(xr + 4 * cc);
-    ww[j] = load4(w + 4 * cc);
-    bb[j] = load4(b + 4 * cc);
-  }
-  if (delta != nullptr) {
+  float4_t ww[MAXC], bb[MAXC];
+  auto load_wb = [&]() {
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
       const int c = lane + j * 64, cc = c < nc ? c : 0;
-      dv[j] = load4(delta + row * d + 4 * cc);
+      ww[j] = load4(w + 4 * cc);
+      bb[j] = load4(b + 4 * cc);
     }
-  }
-  float s = 0.f;
+  };
+  // unconditional loads (lanes past the row end read column 0 and are zeroed): a load under a
+  // divergent `if` gets a vmcnt(0) at the branch join, one HBM round trip per 256-column chunk.
+  // One-row launches load gamma / beta with the row (on gfx950 vmcnt also counts stores: loading
+  // them after the xs stores would wait for those stores to complete).
+  auto one_row = [&](long row) {
+    const TX* xr = x + row * d;
+    float4_t v[MAXC], dv[MAXC];
 #pragma unroll
-  for (int j = 0; j < MAXC; ++j) {
-    const int c = lane + j * 64;
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = lane + j * 64, cc = c < nc ? c : 0;
+      v[j] = load4(xr + 4 * cc);
+    }
+    if (!kPersist) load_wb();
     if (delta != nullptr) {
-      if (dr.thr != 0) {  // residual-branch dropout (reference gpt.py resid/mlp_dropout)
-        const uint64_t e0 = (uint64_t)row * d + 4 * c;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) dv[j][t] = drop_keep(dr.seed, dr.thr, e0 + t) ? dv[j][t] * dr.scale : 0.f;
+      for (int j = 0; j < MAXC; ++j) {
+        const int c = lane + j * 64, cc = c < nc ? c : 0;
+        dv[j] = load4(delta + row * d + 4 * cc);
       }
-      v[j] += dv[j];
-      if (!std::is_same<TX, float>::value) v[j] = round_bf16x4(v[j]);
-      if (c < nc) store4(xs_out + row * d + 4 * c, v[j]);
     }
-    if (c >= nc) v[j] = float4_t{0.f, 0.f, 0.f, 0.f};
-    s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
-  }
-  const float inv_d = 1.f / (float)d;
-  const float mu = wave_sum(s) * inv_d;
-  float q = 0.f;
+    float s = 0.f;
 #pragma unroll
-  for (int j = 0; j < MAXC; ++j) {
-    const int c = lane + j * 64;
-    if (c < nc) {
-      float4_t t = v[j] - mu;
-      q += t[0] * t[0] + t[1] * t[1] + t[2] * t[2] + t[3] * t[3];
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = lane + j * 64;
+      if (delta != nullptr) {
+        if (dr.thr != 0) {  // residual-branch dropout (reference gpt.py resid/mlp_dropout)
+          const uint64_t e0 = (uint64_t)row * d + 4 * c;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) dv[j][t] = drop_keep(dr.seed, dr.thr, e0 + t) ? dv[j][t] * dr.scale : 0.f;
+        }
+        v[j] += dv[j];
+        if (!std::is_same<TX, float>::value) v[j] = round_bf16x4(v[j]);
+        if (c < nc) store4(xs_out + row * d + 4 * c, v[j]);
+      }
+      if (c >= nc) v[j] = float4_t{0.f, 0.f, 0.f, 0.f};
+      s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
     }
-  }
-  const float rs = rsqrtf(wave_sum(q) * inv_d + eps);
+    const float inv_d = 1.f / (float)d;
+    const float mu = wave_sum(s) * inv_d;
+    float q = 0.f;
 #pragma unroll
-  for (int j = 0; j < MAXC; ++j) {
-    const int c = lane + j * 64;
-    const float4_t out = (v[j] - mu) * rs * ww[j] + bb[j];
-    if (c < nc) store4(y + row * d + 4 * c, out);
-  }
-  if (lane == 0) {
-    mean_out[row] = mu;
-    rstd_out[row] = rs;
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = lane + j * 64;
+      if (c < nc) {
+        float4_t t = v[j] - mu;
+        q += t[0] * t[0] + t[1] * t[1] + t[2] * t[2] + t[3] * t[3];
+      }
+    }
+    const float rs = rsqrtf(wave_sum(q) * inv_d + eps);
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = lane + j * 64;
+      const float4_t out = (v[j] - mu) * rs * ww[j] + bb[j];
+      if (c < nc) store4(y + row * d + 4 * c, out);
+    }
+    if (lane == 0) {
+      mean_out[row] = mu;
+      rstd_out[row] = rs;
+    }
+  };
+  const long row0 = (long)blockIdx.x * kLnWaves + (threadIdx.x >> 6);
+  if constexpr (kPersist) {
+    load_wb();
+    for (long row = row0; row < M; row += (long)gridDim.x * kLnWaves) one_row(row);
+  } else {
+    if (row0 < M) one_row(row0);
   }
 }
 
@@ -388,7 +410,8 @@ __global__ __launch_bounds__(256, 3) void ln_bwd_split_kernel(
 
 template <int MAXC, typename TX>
 void launch_fwd_x(const LnFwdArgs& a, hipStream_t st) {
-  dim3 grid((a.M + kLnWaves - 1) / kLnWaves), block(256);
+  const long wgs = (a.M + kLnWaves - 1) / kLnWaves;
+  dim3 grid((unsigned)(ln_fwd_persistent<MAXC>() ? std::min<long>(wgs, 8L * device_cu_count()) : wgs)), block(256);
 #define LN_FWD(TD, TY)                                                                              \
   hipLaunchKernelGGL((add_ln_fwd_kernel<MAXC, TD, TY, TX>), grid, block, 0, st, (const TX*)a.x,     \
                      (const TD*)a.delta, a.w, a.b, (TX*)a.xs_out, (TY*)a.y, a.mean, a.rstd, a.M, a.d, \

@@ -290,9 +290,9 @@ __global__ __launch_bounds__(256, ROWS == 1 ? (MAXC <= 3 ? 4 : 2) : 3) void ln_b
 
 // Split-row backward for wide rows (GPT-2 XL's d = 1600): a workgroup's 4 waves take 2 rows per
 // iteration, each row split into two column halves held by two waves, so a wave keeps half a row
-// (MAXC = 7 -> 4 float4 chunks per lane) and the kernel stays at <= 168 VGPRs — one wave then fits
-// on a SIMD beside the side stream's weight-gradient GEMM (336 of 512 registers), where the
-// whole-row kernel's 256 did not.  The two halves' row sums meet in LDS (one barrier per row
+// (MAXC = 7 -> 4 float4 chunks per lane) and the kernel stays at <= 168 VGPRs (written for the
+// round-2 side stream's weight-gradient GEMM beside it; since round 6 the wave's half of gamma also
+// stays in registers instead of being re-read per row, 164 VGPRs).  The two halves' row sums meet in LDS (one barrier per row
 // pair, parity double-buffered); column partials and the per-wave dproj rows are summed over the
 // two row slots at the end (fixed order).
 template <int MAXC, typename TDY, bool LOWP_OUT, typename TX, typename TG>
@@ -316,11 +316,13 @@ __global__ __launch_bounds__(256, 3) void ln_bwd_split_kernel(
   float* pp = smem + (2 + slot) * d;  // this row slot's dproj partial (this wave's half of it)
 
   float4_t pw[HC], pb[HC];
+  float4_t gam[HC];  // this wave's half of gamma, loaded once (XL: 0.113 -> 0.096 ms, profiles/r6/ln/)
 #pragma unroll
   for (int j = 0; j < HC; ++j) {
     pw[j] = zero; pb[j] = zero;
     const int cl = lane + j * 64;
     if (has_pp && cl < nhalf) store4(pp + 4 * (cbase + cl), zero);
+    gam[j] = load4(w + 4 * (cbase + (cl < nhalf ? cl : 0)));
   }
 
   int par = 0;
@@ -329,7 +331,6 @@ __global__ __launch_bounds__(256, 3) void ln_bwd_split_kernel(
     const bool live = row0 < M;  // wave-uniform
     const long row = live ? row0 : 0;
     const float mu = mean[row], rs = rstd[row];
-    const float* wr = w + __builtin_amdgcn_readfirstlane((int)(row >> 40));
     float4_t g[HC], xh[HC], rr[HC];
 #pragma unroll
     for (int j = 0; j < HC; ++j) {
@@ -351,7 +352,7 @@ __global__ __launch_bounds__(256, 3) void ln_bwd_split_kernel(
       const bool ok = live && cl < nhalf;
       g[j] = ok ? g[j] * scale : zero;
       xh[j] = ok ? (xh[j] - mu) * rs : zero;
-      float4_t gw = g[j] * load4(wr + 4 * c);
+      float4_t gw = g[j] * gam[j];
       s1 += gw[0] + gw[1] + gw[2] + gw[3];
       float4_t gx = gw * xh[j];
       s2 += gx[0] + gx[1] + gx[2] + gx[3];
@@ -368,7 +369,7 @@ __global__ __launch_bounds__(256, 3) void ln_bwd_split_kernel(
 #pragma unroll
     for (int j = 0; j < HC; ++j) {
       const int cl = lane + j * 64, c = cbase + (cl < nhalf ? cl : 0);
-      float4_t out = (g[j] * load4(wr + 4 * c) - c1 - xh[j] * c2) * rs;
+      float4_t out = (g[j] * gam[j] - c1 - xh[j] * c2) * rs;
       if (dresid != nullptr) out += rr[j];
       float4_t br = out;
       if (dr.thr != 0) {

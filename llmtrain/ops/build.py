@@ -1,7 +1,7 @@
 """Build the in-tree HIP extension ``llmtrain/ops/_llmtrain_hip.so`` for gfx950.
 
     python -m llmtrain.ops.build [--jobs N] [--force] [--debug]
-    python -m llmtrain.ops.build --variant NAME -D MACRO[=VALUE] ...   # A/B build of the same sources
+    python -m llmtrain.ops.build --variant NAME -D MACRO[=VALUE] ... [--cflag=-fFLAG]   # A/B build
 
 Every ``csrc/*.hip`` kernel file is compiled by ``hipcc --offload-arch=gfx950`` into its own
 object (these TUs include only the HIP runtime, so they compile in seconds); ``csrc/bindings.cpp``
@@ -88,11 +88,14 @@ def _stale(obj: Path, src: Path) -> bool:
     return any(p.stat().st_mtime > mtime for p in [src, *_headers(), Path(__file__)])
 
 
-def _compile(src: Path, debug: bool, force: bool, objdir: Path = OBJDIR, defines: tuple[str, ...] = ()) -> Path:
+def _compile(src: Path, debug: bool, force: bool, objdir: Path = OBJDIR, defines: tuple[str, ...] = (),
+             cflags: tuple[str, ...] = ()) -> Path:
     obj = objdir / (src.name + (".dbg" if debug else "") + ".o")
     if not force and not _stale(obj, src):
         return obj
     cmd = [_hipcc(), *_common_flags(debug), *(f"-D{d}" for d in defines)]
+    if src.suffix == ".hip":
+        cmd += list(cflags)
     if src.suffix == ".cpp":
         cmd += ["-x", "hip", *_torch_flags()]
     cmd += ["-c", str(src), "-o", str(obj)]
@@ -104,7 +107,7 @@ def _compile(src: Path, debug: bool, force: bool, objdir: Path = OBJDIR, defines
 
 def build(
     *, jobs: int | None = None, force: bool = False, debug: bool = False, verbose: bool = True,
-    variant: str | None = None, defines: tuple[str, ...] = (),
+    variant: str | None = None, defines: tuple[str, ...] = (), cflags: tuple[str, ...] = (),
 ) -> Path:
     """Compile every kernel for gfx950 and link the extension; returns the .so path."""
     objdir = OBJDIR if variant is None else OBJDIR.parent / f"hip_obj_{variant}"
@@ -112,7 +115,7 @@ def build(
     sources = sorted(CSRC.glob("*.hip")) + [CSRC / "bindings.cpp"]
     jobs = jobs or min(16, os.cpu_count() or 4, len(sources))
     with ThreadPoolExecutor(max_workers=jobs) as pool:
-        objs = list(pool.map(lambda s: _compile(s, debug, force, objdir, defines), sources))
+        objs = list(pool.map(lambda s: _compile(s, debug, force, objdir, defines, cflags), sources))
     newest = max(o.stat().st_mtime for o in objs)
     out = OUT_DEBUG if debug else OUT
     if variant is not None:
@@ -142,11 +145,13 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--variant", default=None, help="A/B build name (llmtrain/ops/variants/)")
     ap.add_argument("-D", dest="defines", action="append", default=[], help="extra define for --variant")
+    ap.add_argument("--cflag", dest="cflags", action="append", default=[],
+                    help="extra hipcc flag for the kernel files of a --variant (e.g. -fno-slp-vectorize)")
     args = ap.parse_args(argv)
-    if args.defines and args.variant is None:
-        ap.error("-D needs --variant (the release build takes no extra defines)")
-    build(jobs=args.jobs, force=args.force or bool(args.defines), debug=args.debug, variant=args.variant,
-          defines=tuple(args.defines))
+    if (args.defines or args.cflags) and args.variant is None:
+        ap.error("-D / --cflag need --variant (the release build takes no extra flags)")
+    build(jobs=args.jobs, force=args.force or bool(args.defines) or bool(args.cflags), debug=args.debug,
+          variant=args.variant, defines=tuple(args.defines), cflags=tuple(args.cflags))
     return 0
 
 

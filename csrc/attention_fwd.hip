@@ -35,11 +35,6 @@
 
 #include "attention_common.h"
 
-#ifndef LLMT_ATTN_FWD_SCALAR
-#define LLMT_ATTN_FWD_SCALAR 0  // 1: scalar fp32 exponent args / row sum instead of packed (A/B builds)
-#endif
-
-
 namespace llmt {
 namespace attn {
 
@@ -233,22 +228,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
       // exponent arguments and the row sum in packed fp32 (v_pk_fma_f32 / v_pk_add_f32: half the
       // VALU issue of the scalar forms; the loop is VALU-issue bound).  The sum stays per lane half
       // (this lane's 32 keys of the tile): l_run is joined across the halves once, after the sweep.
-#if LLMT_ATTN_FWD_SCALAR
-      float ps0 = 0.f, ps1 = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const float p0 = __builtin_amdgcn_exp2f(fmaf(s[kt][r], c, -mc));
-          const float p1 = __builtin_amdgcn_exp2f(fmaf(s[kt][r + 1], c, -mc));
-          s[kt][r] = p0;
-          s[kt][r + 1] = p1;
-          ps0 += p0;
-          ps1 += p1;
-        }
-      }
-      const float psum = ps0 + ps1;
-#else
       const f32x2 cc = {c, c}, nmc = {-mc, -mc};
       f32x2 ps = {0.f, 0.f};
 #pragma unroll
@@ -264,7 +243,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
         }
       }
       const float psum = ps[0] + ps[1];
-#endif
       if (DROPOUT) {  // the normaliser sums the undropped P; P V uses the masked, rescaled P
         const uint32_t e_q = (uint32_t)q * (uint32_t)T + (uint32_t)(kbase + 4 * half);
 #pragma unroll

@@ -15,16 +15,21 @@
 //  * the S^T accumulator is converted to bf16 in registers and used directly as the B operand
 //    of O^T += V^T P^T (no LDS round trip for P); V^T fragments come from LDS through the gfx950
 //    transposing read ds_read_b64_tr_b16;
-//  * K/V tiles of 64 keys are double-buffered in LDS with register staging (loads for tile
-//    i+1 are issued before the MFMAs of tile i and written after them: one barrier per tile);
+//  * K/V tiles of 64 keys are double-buffered in LDS and filled by LDS-DMA (buffer_load ... lds;
+//    each lane's source chunk chosen so the image lands swizzled), one tile ahead, one barrier per
+//    tile.  Without staging registers the kernel fits 128 VGPRs, i.e. FOUR workgroups (16 waves)
+//    per CU instead of three: 0.391-0.393 vs 0.406-0.410 ms at GPT-2 124M micro-batch 128,
+//    0.216 vs 0.223-0.231 at XL (profiles/r6/attn/fwd_lds_dma_4wg_ab.txt).  hd = 128 (NH = 2) keeps
+//    register staging two tiles ahead;
 //  * one XOR swizzle of the 16-byte chunks of each 128-byte LDS row makes both the row reads
 //    (ds_read_b128, K as the A operand) and the transposed reads (V) bank-conflict free;
 //  * softmax in the exp2 domain (v_exp_f32), scale folded into one multiply;
 //  * heaviest (last) query blocks of ALL (b, h) are dispatched first to shorten the causal tail;
-//  * measured alternative (commit f15d290): K/V by LDS-DMA into a 4-slot ring with the next
-//    tile's Q K^T MFMAs interleaved into this tile's softmax ran 2-7% SLOWER than this register-
-//    staged body — the loop is bound by VALU issue (~130 VALU per 16 MFMA per wave-tile), which
-//    intra-wave software pipelining cannot remove;
+//  * measured alternatives: K/V by LDS-DMA into a 4-slot ring with the next tile's Q K^T MFMAs
+//    interleaved into this tile's softmax (commit f15d290) ran 2-7% SLOWER than register staging,
+//    and so did a cross-tile pipeline (softmax of tile j beside the S MFMAs of tile j + 1, 8-13%,
+//    docs/round6.md section 18): the loop is bound by VALU issue (~130 VALU per 16 MFMA per
+//    wave-tile), and what pays is more resident waves, not intra-wave pipelining;
 //  * SMALLHD: head dims below 64 (multiples of 8: the reference presets' 32 and 48) run the same
 //    64-wide tiles with the missing dims zero-filled at load time and never stored;
 //  * KMASK: key-padding mask (reference gpt.py:60-64) from one 64-bit word per 64-key tile (a
@@ -69,10 +74,35 @@ constexpr int kFwdWaves = 4;
 constexpr int kQBlk = 32 * kFwdWaves;  // 128 query rows per workgroup
 constexpr int kKBlk = 64;              // keys per LDS tile
 
+// one tile's K and V rows of this wave (2 + 2 one-KiB LDS-DMA ops), M0 saved / restored
+__device__ __forceinline__ void dma_kv(unsigned lds_k, unsigned lds_v, int v0, int v1, __amdgpu_buffer_rsrc_t r,
+                                       int sk, int sv) {
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %[keep], m0\n\t"
+      "s_mov_b32 m0, %[dk]\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[v0], %[r], %[sk] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[v1], %[r], %[sk] offen lds\n\t"
+      "s_mov_b32 m0, %[dv]\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[v0], %[r], %[sv] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[v1], %[r], %[sv] offen lds\n\t"
+      "s_mov_b32 m0, %[keep]"
+      : [keep] "=&s"(keep)
+      : [dk] "s"(lds_k), [dv] "s"(lds_v), [v0] "v"(v0), [v1] "v"(v1), [r] "s"(r), [sk] "s"(sk), [sv] "s"(sv)
+      : "memory", "scc");
+}
+
 // NH: 64-wide halves of the head dim (1: hd <= 64; 2: hd = 128, every [64][128] K/V tile kept as two
 // [64][64] LDS images so the swizzle and fragment readers stay the 64-wide ones)
 template <bool DROPOUT, bool KMASK, bool SMALLHD, int NH = 1>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __restrict__ qkv,
+__global__ __launch_bounds__(256, NH == 1 ? 4 : 2) void attn_fwd_kernel(const bf16_raw* __restrict__ qkv,
                                                           bf16_raw* __restrict__ out,
                                                           float* __restrict__ lse, int T, int H,
                                                           int nqb, DropoutArgs dr, int hd_arg, float c_arg,
@@ -110,6 +140,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
     if (q < T && (!SMALLHD || 16 * kk + 8 * half < hd))
       v = *reinterpret_cast<const ushort8_t*>(base + (long)q * row_stride + 16 * kk + 8 * half);
     qf[kk] = __builtin_bit_cast(bf16x8, v);
+  }
+  if (NH == 1) {
+    // retire the Q loads here: the compiler counts only its own VMEM ops, so a first use of qf inside
+    // the tile loop would get a counted wait there that also drains the in-flight K/V LDS-DMA
+#pragma unroll
+    for (int kk = 0; kk < 4 * NH; ++kk) asm volatile("" : "+v"(qf[kk]));
   }
 
   const int kv_end = min(T, qb * kQBlk + kQBlk);
@@ -156,12 +192,34 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
   const int nkw = (T + kKBlk - 1) / kKBlk;  // key-mask words per sequence
 
   ATTN_PROBE(0);
-  load_tile(st0, 0);
-  store_tile(st0, 0);
-  __syncthreads();
+  constexpr bool kDma = NH == 1;  // K/V by LDS-DMA (hd <= 64); register staging for hd = 128
+  // LDS-DMA fills (kDma): op i of wave w fills rows 8 (2w + i) .. + 7 of the K (V) image, lane l
+  // the 16-byte chunk (l & 7) of row 8 (2w + i) + (l >> 3), i.e. logical chunk (l & 7) ^ g(row)
+  int voff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 8 * (2 * (threadIdx.x >> 6) + i) + (lane >> 3);
+    const int ch = swz(row, lane & 7);
+    voff[i] = (!SMALLHD || ch * 8 < hd) ? (int)((row * row_stride + ch * 8 + hd * H) * 2) : kOobOff;
+  }
+  auto issue = [&](int tile, int buf) {
+    const unsigned dst = (unsigned)(unsigned long)(lds_void*)&smem[buf][0][0][0] + (unsigned)(wave * 2048);
+    const int sk = (int)((long)tile * kKBlk * row_stride * 2);
+    dma_kv(dst, dst + kKBlk * kHD * NH * 2, voff[0], voff[1], rkv, sk, sk + hd * H * 2);
+  };
+  if (kDma) {
+    issue(0, 0);
+    if (ntiles > 1) issue(1, 1);
+    if (ntiles > 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  } else {
+    load_tile(st0, 0);
+    store_tile(st0, 0);
+    __syncthreads();
+    if (ntiles > 1) load_tile(st1, 1);
+    if (ntiles > 2) load_tile(st0, 2);
+  }
   ATTN_PROBE(1);
-  if (ntiles > 1) load_tile(st1, 1);
-  if (ntiles > 2) load_tile(st0, 2);
 
   // iteration `it` computes from LDS buffer it&1, then stages tile it+1 (held in stage set
   // (it+1)&1 since two iterations ago) into the other buffer and refills that set with tile it+3
@@ -269,10 +327,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_raw* __rest
       }
     }
     ATTN_PROBE(2 + 2 * it);
-    if (more) store_tile(st_next, cur ^ 1);
-    __syncthreads();
-    ATTN_PROBE(3 + 2 * it);
-    if (it + 3 < ntiles) load_tile(st_next, it + 3);
+    if (kDma) {  // tile it + 1 landed; every wave is past tile it's buffer: refill it with it + 2
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      ATTN_PROBE(3 + 2 * it);
+      if (it + 2 < ntiles) issue(it + 2, cur);
+    } else {
+      if (more) store_tile(st_next, cur ^ 1);
+      __syncthreads();
+      ATTN_PROBE(3 + 2 * it);
+      if (it + 3 < ntiles) load_tile(st_next, it + 3);
+    }
   };
   for (int it = 0; it < ntiles; it += 2) {
     tile_step(it, st1);

@@ -33,7 +33,8 @@ typedef unsigned short ushort4_t __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 
-// compute units of the current device (queried once per process; every MI355X has 256)
+// compute units of the current device (queried once per process; every MI355X has 256) that grid
+// sizing (persistent kernels, one-round plans) counts on
 inline int device_cu_count() {
   static int n = 0;
   if (n == 0) {

@@ -467,13 +467,11 @@ int bwd_grid_c(const LnBwdArgs& a) {
   static int resident[3][2][2] = {};
   int& per_cu = resident[res_mode(a)][a.dy_bf16 ? 1 : 0][a.dx_lp != nullptr ? 1 : 0];
   if (per_cu == 0) {
-    int n = 0, dev = 0, cus = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    int n = 0;
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bwd_kernel<MAXC>(a), 256, shm);
     // one resident wave of workgroups (mb 32: 1 / 2 / 3 waves 950k / 944k / 936k tok/s, fewer
     // partial rows for the column sums; mb 128 flat: profiles/r2/ab_ln_waves_mb*.txt)
-    per_cu = (n > 0 ? n : 4) * (cus > 0 ? cus : 256);
+    per_cu = (n > 0 ? n : 4) * device_cu_count();
   }
   const int cap = per_cu;
   return stride_grid((long long)(a.M + kBwdWaves - 1) / kBwdWaves, 1, cap);

@@ -59,6 +59,9 @@ CASES = [
     (2, 256, 8, 48, None),  # gpt_wikitext_better head dim
     (3, 200, 2, 32, None),  # ragged T
     (1, 70, 1, 64, None),
+    (2, 8, 4, 16, None),  # gpt_smoke's block size: one partial 64-key tile
+    (3, 33, 2, 64, "mixed"),
+    (1, 2, 2, 64, None),  # (T = 1 makes dQ identically zero: no relative error to check)
     (3, 300, 4, 64, "mixed"),
     (3, 256, 8, 48, "mixed"),
     (4, 128, 8, 32, "mixed"),  # the K8s ConfigMap model's attention with padding
